@@ -1,0 +1,123 @@
+/*
+ * mmpfn_hip.h -- C ABI of the MI355X (gfx950) MMPFN in-context inference engine.
+ *
+ * Plain pointers and sizes only (no torch types).  All data pointers are DEVICE
+ * pointers unless a parameter says "host".  The caller owns input/output buffers;
+ * the context owns packed weights and workspace.  Calls on one context are
+ * serialised on its stream and are asynchronous unless documented otherwise.
+ *
+ * Reference interfaces replaced (paths under too-z/MultiModalPFN/mmpfn/models/mmpfn/):
+ *   mmpfn_create / mmpfn_set_model / mmpfn_load_weight / mmpfn_finalize_weights
+ *       <- model/loading.py:401-542  load_model(): PerFeatureTransformer(...) +
+ *          model.load_state_dict(state_dict, strict=False)
+ *   mmpfn_mixer_forward
+ *       <- model/transformer.py:755-761  self.mgm / self.cap / self.moe applied to image
+ *          (MultiheadGatedMLP :33-57, CrossAttentionPooler :60-88, MoE :91-128)
+ *   mmpfn_forward
+ *       <- model/transformer.py:462-545,555-867  PerFeatureTransformer.forward(
+ *          None, X_full[S,1,F], image_full, y_train[N], single_eval_pos=N,
+ *          only_return_standard_out=True) as called at inference.py:343-348
+ *   mmpfn_embed / mmpfn_run_layers / mmpfn_decode / mmpfn_copy_state
+ *       <- the same forward split at its seams (embedded_input :788,
+ *          transformer_encoder :799-808, decoder :850-853) for parity taps
+ *   mmpfn_item_attention
+ *       <- model/layer.py:341-379 attn_between_items (one token column batch)
+ *   mmpfn_status
+ *       <- model/transformer.py:727-731,790-796 NaN checks (ValueError)
+ */
+#ifndef MMPFN_HIP_H_
+#define MMPFN_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMPFN_OK 0
+#define MMPFN_ERR_INVALID (-1)   /* bad argument / shape */
+#define MMPFN_ERR_HIP (-2)       /* HIP runtime error (see mmpfn_last_error) */
+#define MMPFN_ERR_NAN (-3)       /* NaN in the embedded input (reference raises ValueError) */
+#define MMPFN_ERR_STATE (-4)     /* call order (weights not finalised, ...) */
+#define MMPFN_ERR_WEIGHT (-5)    /* missing / mis-shaped weight */
+
+#define MMPFN_PREC_F32 0  /* parity mode: fp32 everywhere (fp32-input MFMA) */
+#define MMPFN_PREC_BF16 1 /* performance mode: bf16 MFMA operands, fp32 accumulate / residual / LN */
+
+#define MMPFN_MIXER_NONE 0
+#define MMPFN_MIXER_MGM 1
+#define MMPFN_MIXER_MGM_CAP 2
+#define MMPFN_MIXER_MOE 3
+
+typedef struct mmpfn_ctx mmpfn_ctx;
+
+typedef struct mmpfn_model_desc {
+  int emsize;             /* E = 192 */
+  int nhead;              /* 6 (head dim must be 32) */
+  int nlayers;            /* 12 */
+  int nhid;               /* 768 (MLP hidden, decoder hidden, modality width) */
+  int features_per_group; /* model grouping (yaml) */
+  int encoder_features;   /* encoder width nf (checkpoint config.features_per_group) */
+  int n_out;              /* decoder outputs (10) */
+  int mixer_type;         /* MMPFN_MIXER_* */
+  int mgm_heads;          /* MGM heads, or MoE experts */
+  int cap_heads;          /* CAP queries/heads */
+  int two_sets_of_queries;
+  int remove_duplicate_features; /* encoder Linear step index 6 instead of 5 */
+  float ln_eps;           /* 1e-5 */
+  float outlier_sigma;    /* 12 for classification; <= 0 disables soft clipping */
+} mmpfn_model_desc;
+
+/* ---- lifecycle ------------------------------------------------------------------ */
+mmpfn_ctx* mmpfn_create(int device, void* hip_stream);
+void mmpfn_destroy(mmpfn_ctx* ctx);
+const char* mmpfn_last_error(const mmpfn_ctx* ctx);
+int mmpfn_set_stream(mmpfn_ctx* ctx, void* hip_stream);
+const char* mmpfn_version(void);
+
+/* ---- weights (checkpoint ABI: reference state_dict names, fp32 host data) -------- */
+int mmpfn_set_model(mmpfn_ctx* ctx, const mmpfn_model_desc* desc);
+int mmpfn_load_weight(mmpfn_ctx* ctx, const char* name, const float* host_data, int64_t numel);
+int mmpfn_finalize_weights(mmpfn_ctx* ctx); /* pack / fold / convert / upload; synchronous */
+
+/* ---- modality projection heads --------------------------------------------------
+ * image [S][n_mod][nhid] -> tokens [S][C][E]; C = mmpfn_mixer_tokens(ctx, n_mod). */
+int mmpfn_mixer_tokens(const mmpfn_ctx* ctx, int n_mod);
+int mmpfn_mixer_forward(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int precision);
+
+/* ---- one ensemble member's forward ------------------------------------------------
+ * x        [S][F] fp32 (NULL when tabular input is absent)
+ * tokens   [S][C][E] mixer tokens (NULL / C = 0 when there is no image)
+ * y_train  [N] fp32 class codes; uniq [U] sorted unique train codes (after NaN fill)
+ * pos_rand [G + C][E/4]: torch.randn from the model's CPU generator
+ *          (transformer.py:421-424,925-931), G = ceil(F / features_per_group)
+ * logits   [S - N][n_out] fp32 output                                               */
+int mmpfn_forward(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int C, const float* y_train,
+                  int N, const float* uniq, int U, const float* pos_rand, float* logits, int precision);
+
+/* forward split at its seams (parity taps) */
+int mmpfn_embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int C, const float* y_train, int N,
+                const float* uniq, int U, const float* pos_rand, int precision);
+int mmpfn_run_layers(mmpfn_ctx* ctx, int layer_begin, int layer_end);
+int mmpfn_decode(mmpfn_ctx* ctx, float* logits);
+/* copies the current state in reference order [S][T][E] (fp32) */
+int mmpfn_copy_state(mmpfn_ctx* ctx, float* out, int64_t capacity_elems);
+int mmpfn_state_tokens(const mmpfn_ctx* ctx); /* T of the current state */
+
+/* Synchronises the context stream and reports deferred device-side errors
+ * (MMPFN_ERR_NAN when the embedded input held NaNs). */
+int mmpfn_status(mmpfn_ctx* ctx);
+
+/* ---- raw kernels (benchmarks / unit parity) ------------------------------------
+ * Sample-axis attention for one layout batch:
+ *   q  [T][H][S][32], k [T][H][Npad][32], vt [T][H][32][Npad], out [T][S][H*32]
+ *   queries s in [s0, s0+nq) attend keys [0, nk); kv_head_fixed >= 0 forces a KV head.
+ * Element type: fp32 (MMPFN_PREC_F32) or bf16 (MMPFN_PREC_BF16). */
+int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S, int T,
+                         int H, int Npad, int s0, int nq, int nk, int kv_head_fixed, int precision);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MMPFN_HIP_H_ */

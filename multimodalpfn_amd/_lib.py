@@ -1,0 +1,110 @@
+"""ctypes binding of the C-ABI in ``include/mmpfn_hip.h`` (``libmmpfn_hip.so``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C
+multimodalpfn_amd/csrc``).  There is no fallback: if the shared library is missing
+or cannot be loaded, every engine entry point raises ``RuntimeError``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "libmmpfn_hip.so"
+
+MMPFN_OK = 0
+MMPFN_ERR_INVALID = -1
+MMPFN_ERR_HIP = -2
+MMPFN_ERR_NAN = -3
+MMPFN_ERR_STATE = -4
+MMPFN_ERR_WEIGHT = -5
+
+PREC_F32 = 0
+PREC_BF16 = 1
+
+MIXER_NONE, MIXER_MGM, MIXER_MGM_CAP, MIXER_MOE = 0, 1, 2, 3
+MIXER_CODES = {"MGM": MIXER_MGM, "MGM+CAP": MIXER_MGM_CAP, "MoE": MIXER_MOE, None: MIXER_NONE}
+
+
+class ModelDesc(ctypes.Structure):
+    _fields_ = [
+        ("emsize", ctypes.c_int),
+        ("nhead", ctypes.c_int),
+        ("nlayers", ctypes.c_int),
+        ("nhid", ctypes.c_int),
+        ("features_per_group", ctypes.c_int),
+        ("encoder_features", ctypes.c_int),
+        ("n_out", ctypes.c_int),
+        ("mixer_type", ctypes.c_int),
+        ("mgm_heads", ctypes.c_int),
+        ("cap_heads", ctypes.c_int),
+        ("two_sets_of_queries", ctypes.c_int),
+        ("remove_duplicate_features", ctypes.c_int),
+        ("ln_eps", ctypes.c_float),
+        ("outlier_sigma", ctypes.c_float),
+    ]
+
+
+# (name, restype, argtypes) of every symbol the header declares
+_vp, _i, _i64, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+SIGNATURES = [
+    ("mmpfn_create", _vp, [_i, _vp]),
+    ("mmpfn_destroy", None, [_vp]),
+    ("mmpfn_last_error", ctypes.c_char_p, [_vp]),
+    ("mmpfn_set_stream", _i, [_vp, _vp]),
+    ("mmpfn_version", ctypes.c_char_p, []),
+    ("mmpfn_set_model", _i, [_vp, ctypes.POINTER(ModelDesc)]),
+    ("mmpfn_load_weight", _i, [_vp, ctypes.c_char_p, _vp, _i64]),
+    ("mmpfn_finalize_weights", _i, [_vp]),
+    ("mmpfn_mixer_tokens", _i, [_vp, _i]),
+    ("mmpfn_mixer_forward", _i, [_vp, _vp, _i, _i, _vp, _i]),
+    ("mmpfn_forward", _i, [_vp, _vp, _i, _i, _vp, _i, _vp, _i, _vp, _i, _vp, _vp, _i]),
+    ("mmpfn_embed", _i, [_vp, _vp, _i, _i, _vp, _i, _vp, _i, _vp, _i, _vp, _i]),
+    ("mmpfn_run_layers", _i, [_vp, _i, _i]),
+    ("mmpfn_decode", _i, [_vp, _vp]),
+    ("mmpfn_copy_state", _i, [_vp, _vp, _i64]),
+    ("mmpfn_state_tokens", _i, [_vp]),
+    ("mmpfn_status", _i, [_vp]),
+    ("mmpfn_item_attention", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i]),
+]
+
+_LIB = None
+
+
+def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
+    """Load ``libmmpfn_hip.so`` (loud failure, no fallback)."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise RuntimeError(
+            f"MMPFN HIP engine library not found at {p}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (make -C multimodalpfn_amd/csrc)"
+        )
+    # torch must own the HIP runtime first so both resolve the same libamdhip64.so.7
+    import torch  # noqa: F401
+
+    lib = ctypes.CDLL(str(p))
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def check(lib, ctx, rc: int, what: str) -> None:
+    if rc == MMPFN_OK:
+        return
+    msg = lib.mmpfn_last_error(ctx)
+    msg = msg.decode() if msg else ""
+    if rc == MMPFN_ERR_NAN:
+        raise ValueError(f"{what}: {msg}")
+    raise EngineError(f"{what} failed (rc={rc}): {msg}")

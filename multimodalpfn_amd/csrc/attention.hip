@@ -1,0 +1,372 @@
+// Attention kernels of the PerFeatureEncoderLayer (layer.py:332-395,
+// multi_head_attention.py:547-736) for gfx950.
+//
+// 1. attn_feature: self-attention over the T tokens of every row s (feature axis).
+//    T is small (tens to a few hundred); one 256-thread block per row, one thread per
+//    (head, query token), K/V staged through LDS in 32-key chunks, chunked online
+//    softmax in fp32 on the VALU.
+//
+// 2. attn_item: the sample-axis flash attention -- the dominant cost of the forward.
+//    For token column t and head h, query rows s in [s0, s0+nq) attend to keys
+//    [0, nk) (the train rows).  Train queries use their own head's K/V; test queries
+//    use head 0's K/V for every head (reuse_first_head_kv, layer.py:344-358) via
+//    kv_head_fixed = 0.  The scores are computed transposed, S^T = K . Q^T, so the
+//    query index lives on the MFMA lane and the keys in accumulator registers: the
+//    softmax row reductions are in-register (plus one lane^32 exchange) and the
+//    S^T accumulator is fed back as the B operand of O^T += V^T . P^T without any
+//    LDS round trip (cdna_hip_programming.md section 3, "accumulator as operand").
+//    exp2 with log2(e)/sqrt(d) folded into one FMA; the row sum is kept per half-wave
+//    and combined once at the end.
+//      bf16 : v_mfma_f32_32x32x16_bf16 (4 per 32x64 score tile + 4 for P.V)
+//      f32  : v_mfma_f32_32x32x2_f32 (parity mode; exact fp32 fma chains)
+#include "common.h"
+#include "kernels.h"
+
+namespace mmpfn {
+
+namespace {
+
+// ------------------------------------------------------------------ feature attention
+constexpr int FA_KC = 32;  // keys per LDS chunk
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void attn_feature_kernel(const TI* __restrict__ qkv, TO* __restrict__ out,
+                                                           int S, int T, int H) {
+  __shared__ float Ks[6 * FA_KC * 33];  // [H][KC][32+1]
+  __shared__ float Vs[6 * FA_KC * 33];
+  const int s = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t slab = (int64_t)H * T * 32;  // elements per (s, j)
+  const TI* qb = qkv + (int64_t)s * 3 * slab;
+  const TI* kb = qb + slab;
+  const TI* vb = qb + 2 * slab;
+  const float scale = 0.17677669529663687f;  // 1/sqrt(32)
+  const int npairs = H * T;
+  for (int pb = 0; pb < npairs; pb += 256) {
+    const int pair = pb + tid;
+    const bool active = pair < npairs;
+    const int h = active ? pair / T : 0, tq = active ? pair % T : 0;
+    float q[32], acc[32];
+    const TI* qr = qb + ((int64_t)h * T + tq) * 32;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) {
+      q[d] = to_f32(qr[d]) * scale;
+      acc[d] = 0.f;
+    }
+    float m = -INFINITY, l = 0.f;
+    for (int k0 = 0; k0 < T; k0 += FA_KC) {
+      const int kc = min(FA_KC, T - k0);
+      __syncthreads();
+      for (int i = tid; i < H * kc * 32; i += 256) {
+        const int hh = i / (kc * 32), rem = i % (kc * 32), kk = rem >> 5, d = rem & 31;
+        const int64_t gi = ((int64_t)hh * T + k0 + kk) * 32 + d;
+        Ks[(hh * FA_KC + kk) * 33 + d] = to_f32(kb[gi]);
+        Vs[(hh * FA_KC + kk) * 33 + d] = to_f32(vb[gi]);
+      }
+      __syncthreads();
+      if (active) {
+        float sc[FA_KC];
+        float cm = -INFINITY;
+#pragma unroll
+        for (int kk = 0; kk < FA_KC; ++kk) {
+          float a = -INFINITY;
+          if (kk < kc) {
+            const float* kr = Ks + (h * FA_KC + kk) * 33;
+            a = 0.f;
+#pragma unroll
+            for (int d = 0; d < 32; ++d) a = fmaf(q[d], kr[d], a);
+          }
+          sc[kk] = a;
+          cm = fmaxf(cm, a);
+        }
+        const float mn = fmaxf(m, cm);
+        const float corr = expf(m - mn);
+        l *= corr;
+#pragma unroll
+        for (int d = 0; d < 32; ++d) acc[d] *= corr;
+#pragma unroll
+        for (int kk = 0; kk < FA_KC; ++kk) {
+          if (kk < kc) {
+            const float pexp = expf(sc[kk] - mn);
+            l += pexp;
+            const float* vr = Vs + (h * FA_KC + kk) * 33;
+#pragma unroll
+            for (int d = 0; d < 32; ++d) acc[d] = fmaf(pexp, vr[d], acc[d]);
+          }
+        }
+        m = mn;
+      }
+    }
+    if (active) {
+      const float inv = 1.0f / l;
+      TO* orow = out + ((int64_t)tq * S + s) * (H * 32) + h * 32;
+#pragma unroll
+      for (int d = 0; d < 32; ++d) orow[d] = from_f32<TO>(acc[d] * inv);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ item attention
+constexpr int IA_KT = 64;          // keys per LDS tile
+constexpr int IA_QB = 128;         // queries per block (4 waves x 32)
+
+template <bool BF16>
+struct IaLds {
+  static constexpr int KROW = BF16 ? 80 : 144;    // bytes per key row   (32 d + pad)
+  static constexpr int VROW = BF16 ? 136 : 272;   // bytes per V^T row   (64 keys + pad)
+  static constexpr int KBYTES = IA_KT * KROW;
+  static constexpr int VBYTES = 32 * VROW;
+  static constexpr int STAGE = KBYTES + VBYTES;
+};
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__ Qp, const void* __restrict__ Kp,
+                                                        const void* __restrict__ Vp, void* __restrict__ Op, int S,
+                                                        int T, int H, int Npad, int s0, int nq, int nk,
+                                                        int kvh_fixed) {
+  typedef typename std::conditional<BF16, bf16, float>::type TE;
+  constexpr int EB = sizeof(TE);
+  using L = IaLds<BF16>;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * L::STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.y, t = blockIdx.z;
+  const int kvh = kvh_fixed >= 0 ? kvh_fixed : h;
+  const int64_t thq = (int64_t)t * H + h;
+  const int64_t thk = (int64_t)t * H + kvh;
+  const TE* Q = (const TE*)Qp + thq * S * 32;
+  const TE* Kg = (const TE*)Kp + thk * (int64_t)Npad * 32;
+  const TE* Vg = (const TE*)Vp + thk * 32 * (int64_t)Npad;
+  const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
+
+  const int qi = blockIdx.x * IA_QB + wave * 32 + r;  // query offset in [0, nq)
+  const int64_t qs = s0 + min(qi, nq - 1);
+
+  // ---- Q fragments (B operand of S^T = K Q^T)
+  bf16x8 qb[2];
+  float qf[16];
+  if constexpr (BF16) {
+    const bf16* qrow = (const bf16*)Q + qs * 32;
+    qb[0] = *(const bf16x8*)(qrow + 8 * hh);
+    qb[1] = *(const bf16x8*)(qrow + 16 + 8 * hh);
+  } else {
+    const float* qrow = (const float*)Q + qs * 32 + 16 * hh;
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) *(f32x4*)(qf + i) = *(const f32x4*)(qrow + i);
+  }
+
+  // ---- staging: K tile [64][32], V^T tile [32][64]
+  constexpr int KCH = IA_KT * 32 * EB / 16 / 256;  // 16-byte chunks per thread (K)
+  constexpr int VCH = 32 * IA_KT * EB / 16 / 256;
+  u32x4 rk[KCH], rv[VCH];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) {
+      const int cidx = tid + 256 * i;  // chunk over the contiguous K tile
+      rk[i] = *(const u32x4*)((const unsigned char*)(Kg + (int64_t)k0 * 32) + cidx * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < VCH; ++i) {
+      const int cidx = tid + 256 * i;
+      constexpr int CPR = IA_KT * EB / 16;  // chunks per V^T row
+      const int d = cidx / CPR, ch = cidx % CPR;
+      rv[i] = *(const u32x4*)((const unsigned char*)(Vg + (int64_t)d * Npad + k0) + ch * 16);
+      // zero V for keys >= nk so masked (p = 0) columns never meet stale NaN/inf
+      constexpr int EPC = 16 / EB;
+      const int kfirst = k0 + ch * EPC;
+      if (kfirst + EPC > nk) {
+        if constexpr (BF16) {
+          bf16x8 e = __builtin_bit_cast(bf16x8, rv[i]);
+#pragma unroll
+          for (int j = 0; j < EPC; ++j)
+            if (kfirst + j >= nk) e[j] = (bf16)0.0f;
+          rv[i] = __builtin_bit_cast(u32x4, e);
+        } else {
+          f32x4 e = __builtin_bit_cast(f32x4, rv[i]);
+#pragma unroll
+          for (int j = 0; j < EPC; ++j)
+            if (kfirst + j >= nk) e[j] = 0.0f;
+          rv[i] = __builtin_bit_cast(u32x4, e);
+        }
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    unsigned char* Ks = lds + buf * L::STAGE;
+    unsigned char* Vs = Ks + L::KBYTES;
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) {
+      const int cidx = tid + 256 * i;
+      constexpr int CPR = 32 * EB / 16;  // chunks per K row
+      const int row = cidx / CPR, ch = cidx % CPR;
+      *(u32x4*)(Ks + row * L::KROW + ch * 16) = rk[i];
+    }
+#pragma unroll
+    for (int i = 0; i < VCH; ++i) {
+      const int cidx = tid + 256 * i;
+      constexpr int CPR = IA_KT * EB / 16;
+      const int d = cidx / CPR, ch = cidx % CPR;
+      unsigned char* dst = Vs + d * L::VROW + ch * 16;
+      if constexpr (BF16) {  // 136-byte rows are 8-byte aligned only
+        *(u32x2*)dst = u32x2{rv[i].x, rv[i].y};
+        *(u32x2*)(dst + 8) = u32x2{rv[i].z, rv[i].w};
+      } else {
+        *(u32x4*)dst = rv[i];
+      }
+    }
+  };
+
+  f32x16 o;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) o[i] = 0.f;
+  float m = -INFINITY, lsum = 0.f;
+
+  const int ntiles = (nk + IA_KT - 1) / IA_KT;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int it = 0; it < ntiles; ++it) {
+    const int k0 = it * IA_KT;
+    if (it + 1 < ntiles) gload(k0 + IA_KT);
+    const unsigned char* Ks = lds + (it & 1) * L::STAGE;
+    const unsigned char* Vs = Ks + L::KBYTES;
+
+    // ---- S^T for the two 32-key subtiles
+    f32x16 sacc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[u][i] = 0.f;
+      const unsigned char* krow = Ks + (32 * u + r) * L::KROW;
+      if constexpr (BF16) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 ka = *(const bf16x8*)(krow + (16 * ks + 8 * hh) * 2);
+          sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qb[ks], sacc[u], 0, 0, 0);
+        }
+      } else {
+        float kf[16];
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) *(f32x4*)(kf + i) = *(const f32x4*)(krow + (16 * hh + i) * 4);
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks)
+          sacc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[ks], qf[ks], sacc[u], 0, 0, 0);
+      }
+    }
+    // ---- mask keys >= nk (only in the last tile)
+    if (k0 + IA_KT > nk) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = k0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (key >= nk) sacc[u][i] = -INFINITY;
+        }
+    }
+    // ---- online softmax (row = this lane's query; partner lane^32 holds the other keys)
+    float tm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) tm = fmaxf(tm, sacc[u][i]);
+    tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+    const float mn = fmaxf(m, tm);
+    const float alpha = exp2f((m - mn) * c);
+    const float mc = mn * c;
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pv = exp2f(fmaf(sacc[u][i], c, -mc));
+        sacc[u][i] = pv;
+        ps += pv;
+      }
+    lsum = lsum * alpha + ps;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[i] *= alpha;
+
+    // ---- O^T += V^T . P^T
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const unsigned char* vrow = Vs + r * L::VROW;
+      if constexpr (BF16) {
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          bf16x8 pb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[j] = (bf16)sacc[u][8 * sp + j];
+          const int kb = 32 * u + 16 * sp + 4 * hh;
+          const u32x2 v0 = *(const u32x2*)(vrow + kb * 2);
+          const u32x2 v1 = *(const u32x2*)(vrow + (kb + 8) * 2);
+          const bf16x8 va = __builtin_bit_cast(bf16x8, u32x4{v0.x, v0.y, v1.x, v1.y});
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 vv = *(const f32x4*)(vrow + (32 * u + 8 * g + 4 * hh) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o = __builtin_amdgcn_mfma_f32_32x32x2f32(vv[e], sacc[u][4 * g + e], o, 0, 0, 0);
+        }
+      }
+    }
+    if (it + 1 < ntiles) lstore((it + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- normalise and store O[t][s][h*32 + d]
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const float inv = 1.0f / ltot;
+  if (qi < nq) {
+    TE* orow = (TE*)Op + ((int64_t)t * S + qs) * (H * 32) + h * 32;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * hh;
+      if constexpr (BF16) {
+        bf16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = (bf16)(o[4 * g + e] * inv);
+        *(bf16x4*)(orow + d) = w;
+      } else {
+        f32x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = o[4 * g + e] * inv;
+        *(f32x4*)(orow + d) = w;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_attn_feature(const void* qkv, void* out, int S, int T, int H, int prec, hipStream_t st) {
+  if (S <= 0) return hipSuccess;
+  if (H > 6) return hipErrorInvalidValue;
+  if (prec == PREC_BF16)
+    hipLaunchKernelGGL((attn_feature_kernel<bf16, bf16>), dim3(S), dim3(256), 0, st, (const bf16*)qkv, (bf16*)out,
+                       S, T, H);
+  else
+    hipLaunchKernelGGL((attn_feature_kernel<float, float>), dim3(S), dim3(256), 0, st, (const float*)qkv,
+                       (float*)out, S, T, H);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
+                            int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  if (nk <= 0 || Npad % IA_KT != 0 || nk > Npad) return hipErrorInvalidValue;
+  dim3 grid((nq + IA_QB - 1) / IA_QB, H, T);
+  if (prec == PREC_BF16)
+    hipLaunchKernelGGL((attn_item_kernel<true>), grid, dim3(256), 0, st, q, k, vt, out, S, T, H, Npad, s0, nq, nk,
+                       kv_head_fixed);
+  else
+    hipLaunchKernelGGL((attn_item_kernel<false>), grid, dim3(256), 0, st, q, k, vt, out, S, T, H, Npad, s0, nq, nk,
+                       kv_head_fixed);
+  return hipGetLastError();
+}
+
+}  // namespace mmpfn

@@ -1,0 +1,735 @@
+// C ABI of the MMPFN engine: context, weight packing (checkpoint ABI) and the
+// native orchestration of one ensemble member's PerFeatureTransformer forward.
+//
+// Forward (transformer.py:555-867) per member, all on the context stream:
+//   pos-emb  -> x encoder (+pos-emb) -> mixer tokens (+pos-emb) -> y token
+//   -> nlayers x [feature attn | item attn | MLP] (layer.py:272-457)
+//   -> decoder on the test rows of the target token.
+// State layout in HBM: X[T][S][E] fp32 (token-major), so every token column of the
+// sample-axis attention is a contiguous [S][E] slab.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/mmpfn_hip.h"
+#include "kernels.h"
+
+using namespace mmpfn;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct LayerW {  // packed per layer, [N][K] row-major
+  DevBuf feat_qkv, feat_out, item_qkv, item_qtest, item_out, mlp1, mlp2;  // fp32
+  DevBuf feat_qkv_h, feat_out_h, item_qkv_h, item_qtest_h, item_out_h, mlp1_h, mlp2_h;  // bf16
+};
+
+uint16_t f2bf(float f) {  // round-to-nearest-even, NaN preserving
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffff) > 0x7f800000) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fff + ((u >> 16) & 1);
+  return (uint16_t)(u >> 16);
+}
+
+}  // namespace
+
+struct mmpfn_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bool have_model = false, finalized = false;
+  mmpfn_model_desc d{};
+  std::map<std::string, std::vector<float>> host;
+  std::vector<DevBuf> owned;
+
+  std::vector<LayerW> layers;
+  DevBuf enc_w, y_w, y_b, pe_w, pe_b, dec_w1, dec_b1, dec_w2, dec_b2;
+  // mixer
+  DevBuf mgm_w1, mgm_w1_h, mgm_b1, mgm_w2, mgm_w2_h, mgm_b2;
+  DevBuf cap_qp, cap_kv, cap_kv_h, cap_kv_b, cap_o, cap_o_h, cap_o_b, cap_f0, cap_f0_h, cap_f0_b, cap_f3, cap_f3_h,
+      cap_f3_b, cap_ng, cap_nb;
+  DevBuf moe_w1, moe_w1_h, moe_b1, moe_w2, moe_w2_h, moe_b2, moe_gw, moe_gb;
+
+  // workspace
+  DevBuf ws_X, ws_O, ws_big, ws_pe, ws_slots, ws_scr, ws_flag;
+  DevBuf mx[8];
+  // current forward geometry
+  int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0;
+  bool embedded = false;
+};
+
+namespace {
+
+int fail(mmpfn_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess) return fail(ctx, MMPFN_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+int ensure(mmpfn_ctx* ctx, DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes && b.p) return MMPFN_OK;
+  if (b.p) HIPCHK(hipFree(b.p));
+  b.p = nullptr;
+  b.bytes = 0;
+  bytes = (bytes + 255) & ~size_t(255);
+  HIPCHK(hipMalloc(&b.p, bytes));
+  b.bytes = bytes;
+  return MMPFN_OK;
+}
+
+int upload(mmpfn_ctx* ctx, DevBuf& b, const std::vector<float>& v, bool as_bf16) {
+  if (as_bf16) {
+    std::vector<uint16_t> h(v.size());
+    for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf(v[i]);
+    int rc = ensure(ctx, b, h.size() * 2);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(b.p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  } else {
+    int rc = ensure(ctx, b, v.size() * 4);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(b.p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+  }
+  return MMPFN_OK;
+}
+
+const std::vector<float>* getw(mmpfn_ctx* ctx, const std::string& name, size_t numel) {
+  auto it = ctx->host.find(name);
+  if (it == ctx->host.end()) {
+    ctx->err = "missing weight: " + name;
+    return nullptr;
+  }
+  if (it->second.size() != numel) {
+    ctx->err = "weight " + name + " has " + std::to_string(it->second.size()) + " elements, expected " +
+               std::to_string(numel);
+    return nullptr;
+  }
+  return &it->second;
+}
+
+#define GETW(var, name, n)                                  \
+  const std::vector<float>* var = getw(ctx, (name), (n));  \
+  if (!var) return MMPFN_ERR_WEIGHT;
+
+// w_out [H][d][E] -> W[e][h*d+dd]
+std::vector<float> transpose_out(const std::vector<float>& w, int HD, int E) {
+  std::vector<float> o((size_t)E * HD);
+  for (int i = 0; i < HD; ++i)
+    for (int e = 0; e < E; ++e) o[(size_t)e * HD + i] = w[(size_t)i * E + e];
+  return o;
+}
+
+int up2(mmpfn_ctx* ctx, DevBuf& f, DevBuf& h, const std::vector<float>& v) {
+  int rc = upload(ctx, f, v, false);
+  if (rc) return rc;
+  return upload(ctx, h, v, true);
+}
+
+// fold a preceding LayerNorm affine (g, b over K inputs) into Linear (W [N][K], c [N])
+void fold_ln(std::vector<float>& W, std::vector<float>& c, const float* g, const float* b, int N, int K) {
+  for (int n = 0; n < N; ++n) {
+    double acc = c[n];
+    for (int k = 0; k < K; ++k) {
+      acc += (double)W[(size_t)n * K + k] * b[k];
+      W[(size_t)n * K + k] *= g[k];
+    }
+    c[n] = (float)acc;
+  }
+}
+
+int finalize(mmpfn_ctx* ctx) {
+  const mmpfn_model_desc& d = ctx->d;
+  const int E = d.emsize, H = d.nhead, HD = E, Fh = d.nhid, nf = d.encoder_features;
+  ctx->layers.assign(d.nlayers, LayerW{});
+  for (int l = 0; l < d.nlayers; ++l) {
+    const std::string p = "transformer_encoder.layers." + std::to_string(l) + ".";
+    LayerW& L = ctx->layers[l];
+    int rc;
+    GETW(fq, p + "self_attn_between_features._w_qkv", (size_t)3 * HD * E);
+    GETW(fo, p + "self_attn_between_features._w_out", (size_t)HD * E);
+    GETW(io, p + "self_attn_between_items._w_out", (size_t)HD * E);
+    GETW(m1, p + "mlp.linear1.weight", (size_t)Fh * E);
+    GETW(m2, p + "mlp.linear2.weight", (size_t)E * Fh);
+    if ((rc = up2(ctx, L.feat_qkv, L.feat_qkv_h, *fq))) return rc;
+    if ((rc = up2(ctx, L.feat_out, L.feat_out_h, transpose_out(*fo, HD, E)))) return rc;
+    if ((rc = up2(ctx, L.item_out, L.item_out_h, transpose_out(*io, HD, E)))) return rc;
+    if ((rc = up2(ctx, L.mlp1, L.mlp1_h, *m1))) return rc;
+    if ((rc = up2(ctx, L.mlp2, L.mlp2_h, *m2))) return rc;
+    std::vector<float> wtrain((size_t)3 * HD * E), wtest((size_t)HD * E);
+    if (d.two_sets_of_queries) {
+      GETW(wq, p + "self_attn_between_items._w_q", (size_t)2 * HD * E);
+      GETW(wkv, p + "self_attn_between_items._w_kv", (size_t)2 * HD * E);
+      std::copy(wq->begin(), wq->begin() + (size_t)HD * E, wtrain.begin());
+      std::copy(wkv->begin(), wkv->end(), wtrain.begin() + (size_t)HD * E);
+      std::copy(wq->begin() + (size_t)HD * E, wq->end(), wtest.begin());
+    } else {
+      GETW(wqkv, p + "self_attn_between_items._w_qkv", (size_t)3 * HD * E);
+      wtrain = *wqkv;
+      std::copy(wqkv->begin(), wqkv->begin() + (size_t)HD * E, wtest.begin());
+    }
+    if ((rc = up2(ctx, L.item_qkv, L.item_qkv_h, wtrain))) return rc;
+    if ((rc = up2(ctx, L.item_qtest, L.item_qtest_h, wtest))) return rc;
+  }
+  int rc;
+  {
+    const std::string en = d.remove_duplicate_features ? "encoder.6.layer.weight" : "encoder.5.layer.weight";
+    GETW(w, en, (size_t)E * 2 * nf);
+    if ((rc = upload(ctx, ctx->enc_w, *w, false))) return rc;
+    GETW(yw, "y_encoder.2.layer.weight", (size_t)E * 2);
+    GETW(yb, "y_encoder.2.layer.bias", (size_t)E);
+    if ((rc = upload(ctx, ctx->y_w, *yw, false))) return rc;
+    if ((rc = upload(ctx, ctx->y_b, *yb, false))) return rc;
+    GETW(pw, "feature_positional_embedding_embeddings.weight", (size_t)E * (E / 4));
+    GETW(pb, "feature_positional_embedding_embeddings.bias", (size_t)E);
+    if ((rc = upload(ctx, ctx->pe_w, *pw, false))) return rc;
+    if ((rc = upload(ctx, ctx->pe_b, *pb, false))) return rc;
+    GETW(dw1, "decoder_dict.standard.0.weight", (size_t)Fh * E);
+    GETW(db1, "decoder_dict.standard.0.bias", (size_t)Fh);
+    GETW(dw2, "decoder_dict.standard.2.weight", (size_t)d.n_out * Fh);
+    GETW(db2, "decoder_dict.standard.2.bias", (size_t)d.n_out);
+    if ((rc = upload(ctx, ctx->dec_w1, *dw1, false))) return rc;
+    if ((rc = upload(ctx, ctx->dec_b1, *db1, false))) return rc;
+    if ((rc = upload(ctx, ctx->dec_w2, *dw2, false))) return rc;
+    if ((rc = upload(ctx, ctx->dec_b2, *db2, false))) return rc;
+  }
+  const int D = d.nhid;
+  if (d.mixer_type == MMPFN_MIXER_MGM || d.mixer_type == MMPFN_MIXER_MGM_CAP) {
+    const int mg = d.mgm_heads;
+    std::vector<float> W1((size_t)mg * D * D), B1((size_t)mg * D), W2((size_t)mg * E * (D / 2)),
+        B2((size_t)mg * E);
+    for (int h = 0; h < mg; ++h) {
+      const std::string p = "mgm.projs." + std::to_string(h) + ".";
+      GETW(g, p + "0.weight", (size_t)D);
+      GETW(b, p + "0.bias", (size_t)D);
+      GETW(w1, p + "1.weight", (size_t)D * D);
+      GETW(b1, p + "1.bias", (size_t)D);
+      GETW(w2, p + "4.weight", (size_t)E * (D / 2));
+      GETW(b2, p + "4.bias", (size_t)E);
+      std::vector<float> w = *w1, c = *b1;
+      fold_ln(w, c, g->data(), b->data(), D, D);
+      // interleave GLU halves in 16-row blocks: [a 16i..16i+15 | b 16i..16i+15] per 32 rows
+      for (int i = 0; i < D / 32; ++i)
+        for (int r = 0; r < 32; ++r) {
+          const int src = r < 16 ? 16 * i + r : D / 2 + 16 * i + (r - 16);
+          const size_t dst = (size_t)h * D + 32 * i + r;
+          std::memcpy(&W1[dst * D], &w[(size_t)src * D], D * sizeof(float));
+          B1[dst] = c[src];
+        }
+      std::copy(w2->begin(), w2->end(), W2.begin() + (size_t)h * E * (D / 2));
+      std::copy(b2->begin(), b2->end(), B2.begin() + (size_t)h * E);
+    }
+    if ((rc = up2(ctx, ctx->mgm_w1, ctx->mgm_w1_h, W1))) return rc;
+    if ((rc = upload(ctx, ctx->mgm_b1, B1, false))) return rc;
+    if ((rc = up2(ctx, ctx->mgm_w2, ctx->mgm_w2_h, W2))) return rc;
+    if ((rc = upload(ctx, ctx->mgm_b2, B2, false))) return rc;
+  }
+  if (d.mixer_type == MMPFN_MIXER_MGM_CAP) {
+    const int cap = d.cap_heads;
+    GETW(qs, "cap.queries", (size_t)cap * E);
+    GETW(qpw, "cap.q_proj.weight", (size_t)E * E);
+    GETW(inw, "cap.mha.in_proj_weight", (size_t)3 * E * E);
+    GETW(inb, "cap.mha.in_proj_bias", (size_t)3 * E);
+    GETW(ow, "cap.mha.out_proj.weight", (size_t)E * E);
+    GETW(ob, "cap.mha.out_proj.bias", (size_t)E);
+    GETW(kg, "cap.k_norm.weight", (size_t)E);
+    GETW(kb, "cap.k_norm.bias", (size_t)E);
+    GETW(qg, "cap.q_norm.weight", (size_t)E);
+    GETW(qb, "cap.q_norm.bias", (size_t)E);
+    GETW(ng, "cap.out_norm.weight", (size_t)E);
+    GETW(nb, "cap.out_norm.bias", (size_t)E);
+    GETW(f0w, "cap.ffn.0.weight", (size_t)2 * E * E);
+    GETW(f0b, "cap.ffn.0.bias", (size_t)2 * E);
+    GETW(f3w, "cap.ffn.3.weight", (size_t)2 * E * E);
+    GETW(f3b, "cap.ffn.3.bias", (size_t)E);
+    // weight-only query path: in_proj_q(q_proj(q_norm(queries)))  (transformer.py:81)
+    std::vector<float> qp((size_t)cap * E);
+    for (int c = 0; c < cap; ++c) {
+      const float* q = qs->data() + (size_t)c * E;
+      double mu = 0, var = 0;
+      for (int e = 0; e < E; ++e) mu += q[e];
+      mu /= E;
+      for (int e = 0; e < E; ++e) var += (q[e] - mu) * (q[e] - mu);
+      var /= E;
+      const double inv = 1.0 / std::sqrt(var + d.ln_eps);
+      std::vector<double> qn(E), qq(E);
+      for (int e = 0; e < E; ++e) qn[e] = (q[e] - mu) * inv * (*qg)[e] + (*qb)[e];
+      for (int o = 0; o < E; ++o) {
+        double a = 0;
+        for (int e = 0; e < E; ++e) a += (*qpw)[(size_t)o * E + e] * qn[e];
+        qq[o] = a;
+      }
+      for (int o = 0; o < E; ++o) {
+        double a = (*inb)[o];
+        for (int e = 0; e < E; ++e) a += (*inw)[(size_t)o * E + e] * qq[e];
+        qp[(size_t)c * E + o] = (float)a;
+      }
+    }
+    if ((rc = upload(ctx, ctx->cap_qp, qp, false))) return rc;
+    // K/V in-projection with k_norm's affine folded in (k = v = k_norm(src))
+    std::vector<float> wkv(inw->begin() + (size_t)E * E, inw->end());
+    std::vector<float> bkv(inb->begin() + E, inb->end());
+    fold_ln(wkv, bkv, kg->data(), kb->data(), 2 * E, E);
+    if ((rc = up2(ctx, ctx->cap_kv, ctx->cap_kv_h, wkv))) return rc;
+    if ((rc = upload(ctx, ctx->cap_kv_b, bkv, false))) return rc;
+    if ((rc = up2(ctx, ctx->cap_o, ctx->cap_o_h, *ow))) return rc;
+    if ((rc = upload(ctx, ctx->cap_o_b, *ob, false))) return rc;
+    if ((rc = up2(ctx, ctx->cap_f0, ctx->cap_f0_h, *f0w))) return rc;
+    if ((rc = upload(ctx, ctx->cap_f0_b, *f0b, false))) return rc;
+    if ((rc = up2(ctx, ctx->cap_f3, ctx->cap_f3_h, *f3w))) return rc;
+    if ((rc = upload(ctx, ctx->cap_f3_b, *f3b, false))) return rc;
+    if ((rc = upload(ctx, ctx->cap_ng, *ng, false))) return rc;
+    if ((rc = upload(ctx, ctx->cap_nb, *nb, false))) return rc;
+  }
+  if (d.mixer_type == MMPFN_MIXER_MOE) {
+    const int ne = d.mgm_heads;
+    std::vector<float> W1((size_t)ne * (D / 2) * D), B1((size_t)ne * (D / 2)), W2((size_t)ne * E * (D / 2)),
+        B2((size_t)ne * E);
+    for (int i = 0; i < ne; ++i) {
+      const std::string p = "moe.experts." + std::to_string(i) + ".";
+      GETW(g, p + "0.weight", (size_t)D);
+      GETW(b, p + "0.bias", (size_t)D);
+      GETW(w1, p + "1.weight", (size_t)(D / 2) * D);
+      GETW(b1, p + "1.bias", (size_t)D / 2);
+      GETW(w2, p + "4.weight", (size_t)E * (D / 2));
+      GETW(b2, p + "4.bias", (size_t)E);
+      std::vector<float> w = *w1, c = *b1;
+      fold_ln(w, c, g->data(), b->data(), D / 2, D);
+      std::copy(w.begin(), w.end(), W1.begin() + (size_t)i * (D / 2) * D);
+      std::copy(c.begin(), c.end(), B1.begin() + (size_t)i * (D / 2));
+      std::copy(w2->begin(), w2->end(), W2.begin() + (size_t)i * E * (D / 2));
+      std::copy(b2->begin(), b2->end(), B2.begin() + (size_t)i * E);
+    }
+    GETW(gw, "moe.gate.weight", (size_t)ne * D);
+    GETW(gb, "moe.gate.bias", (size_t)ne);
+    if ((rc = up2(ctx, ctx->moe_w1, ctx->moe_w1_h, W1))) return rc;
+    if ((rc = upload(ctx, ctx->moe_b1, B1, false))) return rc;
+    if ((rc = up2(ctx, ctx->moe_w2, ctx->moe_w2_h, W2))) return rc;
+    if ((rc = upload(ctx, ctx->moe_b2, B2, false))) return rc;
+    if ((rc = upload(ctx, ctx->moe_gw, *gw, false))) return rc;
+    if ((rc = upload(ctx, ctx->moe_gb, *gb, false))) return rc;
+  }
+  HIPCHK(hipDeviceSynchronize());
+  return MMPFN_OK;
+}
+
+inline const void* W(const DevBuf& f, const DevBuf& h, int prec) { return prec == PREC_BF16 ? h.p : f.p; }
+
+GemmArgs gargs() {
+  GemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.a_rdiv = 1ll << 62;
+  a.a_rmul = 0;
+  a.rdiv2 = 1ll << 62;
+  a.ln_eps = 1e-5f;
+  return a;
+}
+
+#define RC(expr)                 \
+  do {                           \
+    int rc_ = (expr);            \
+    if (rc_ != MMPFN_OK) return rc_; \
+  } while (0)
+
+int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int C, const float* y, int N,
+          const float* uniq, int U, const float* pos_rand, int prec) {
+  const mmpfn_model_desc& d = ctx->d;
+  if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
+  if (S <= 0 || N <= 0 || N > S || (x && F <= 0) || C < 0 || U <= 0)
+    return fail(ctx, MMPFN_ERR_INVALID, "bad forward geometry");
+  if (!x && C == 0) return fail(ctx, MMPFN_ERR_INVALID, "no input tokens");
+  if (prec != PREC_F32 && prec != PREC_BF16) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  const int E = d.emsize, fpg = d.features_per_group;
+  const int G = x ? (F + fpg - 1) / fpg : 0;
+  const int T = G + C + 1;
+  const int Npad = (N + 63) / 64 * 64;
+  ctx->S = S, ctx->T = T, ctx->N = N, ctx->G = G, ctx->C = C, ctx->Npad = Npad, ctx->prec = prec;
+  const size_t R = (size_t)S * T;
+  RC(ensure(ctx, ctx->ws_X, R * E * 4));
+  RC(ensure(ctx, ctx->ws_O, R * E * 4));
+  const size_t big = std::max(R * d.nhid, R * E + (size_t)2 * T * Npad * E) * 4;
+  RC(ensure(ctx, ctx->ws_big, big));
+  RC(ensure(ctx, ctx->ws_pe, (size_t)(G + C + 1) * E * 4));
+  RC(ensure(ctx, ctx->ws_slots, (size_t)(G + 1) * fpg * sizeof(SlotParams)));
+  RC(ensure(ctx, ctx->ws_scr, 256));
+  RC(ensure(ctx, ctx->ws_flag, 256));
+  hipStream_t st = ctx->stream;
+  float* X = (float*)ctx->ws_X.p;
+  int* flag = (int*)ctx->ws_flag.p;
+  HIPCHK(hipMemsetAsync(flag, 0, 4, st));
+  HIPCHK(launch_pos_emb(pos_rand, G + C, (const float*)ctx->pe_w.p, (const float*)ctx->pe_b.p, (float*)ctx->ws_pe.p, E,
+                        st));
+  if (G) {
+    HIPCHK(launch_encode_x(x, S, F, N, G, fpg, d.encoder_features, d.outlier_sigma, (SlotParams*)ctx->ws_slots.p,
+                           (const float*)ctx->enc_w.p, (const float*)ctx->ws_pe.p, X, E, flag, st));
+  }
+  if (C) {
+    HIPCHK(launch_add_tokens(tokens, S, C, (const float*)ctx->ws_pe.p + (size_t)G * E, X + (size_t)G * S * E, E,
+                             flag, st));
+  }
+  HIPCHK(launch_encode_y(y, N, S, uniq, U, (const float*)ctx->y_w.p, (const float*)ctx->y_b.p,
+                         X + (size_t)(T - 1) * S * E, E, (float*)ctx->ws_scr.p, flag, st));
+  ctx->embedded = true;
+  return MMPFN_OK;
+}
+
+int run_layer(mmpfn_ctx* ctx, int l) {
+  const mmpfn_model_desc& d = ctx->d;
+  const LayerW& L = ctx->layers[l];
+  const int S = ctx->S, T = ctx->T, N = ctx->N, Npad = ctx->Npad, prec = ctx->prec;
+  const int E = d.emsize, H = d.nhead, Q = S - N;
+  const int64_t R = (int64_t)S * T;
+  const bool bf = prec == PREC_BF16;
+  const int eb = bf ? 2 : 4;
+  hipStream_t st = ctx->stream;
+  float* X = (float*)ctx->ws_X.p;
+  void* O = ctx->ws_O.p;
+  unsigned char* big = (unsigned char*)ctx->ws_big.p;
+
+  // ---- attention between features (layer.py:332-339)
+  {
+    GemmArgs a = gargs();
+    a.A = X, a.lda = E, a.a_rdiv = S, a.a_rmul = S;
+    a.W = W(L.feat_qkv, L.feat_qkv_h, prec);
+    a.M = (int)R, a.N = 3 * E, a.K = E;
+    a.q = big, a.S = S, a.T = T, a.H = H;
+    HIPCHK(launch_gemm(a, prec, EPI_FEAT_QKV, true, !bf, 1, st));
+    HIPCHK(launch_attn_feature(big, O, S, T, H, prec, st));
+    GemmArgs b = gargs();
+    b.A = O, b.lda = E, b.W = W(L.feat_out, L.feat_out_h, prec);
+    b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
+    HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
+  }
+  // ---- attention between items (layer.py:341-379)
+  {
+    void* Qi = big;
+    void* Ki = big + (size_t)R * E * eb;
+    void* Vi = (unsigned char*)Ki + (size_t)T * H * Npad * 32 * eb;
+    GemmArgs a = gargs();
+    a.A = X, a.lda = E, a.a_rdiv = N, a.a_rmul = S, a.a_roff = 0;
+    a.W = W(L.item_qkv, L.item_qkv_h, prec);
+    a.M = T * N, a.N = 3 * E, a.K = E;
+    a.q = Qi, a.k = Ki, a.v = Vi, a.S = S, a.Npad = Npad, a.T = T, a.H = H;
+    HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+    if (Q > 0) {
+      GemmArgs c = a;
+      c.a_rdiv = Q, c.a_roff = N;
+      c.W = W(L.item_qtest, L.item_qtest_h, prec);
+      c.M = T * Q, c.N = E;
+      HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+    }
+    HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, T, H, Npad, 0, N, N, -1, prec, st));
+    if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, T, H, Npad, N, Q, N, 0, prec, st));
+    GemmArgs b = gargs();
+    b.A = O, b.lda = E, b.W = W(L.item_out, L.item_out_h, prec);
+    b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
+    HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
+  }
+  // ---- MLP (mlp.py:93-104)
+  {
+    GemmArgs a = gargs();
+    a.A = X, a.lda = E, a.W = W(L.mlp1, L.mlp1_h, prec);
+    a.M = (int)R, a.N = d.nhid, a.K = E, a.act = ACT_GELU;
+    a.C = big, a.ldc = d.nhid;
+    HIPCHK(launch_gemm(a, prec, EPI_STORE, true, !bf, 1, st));
+    GemmArgs b = gargs();
+    b.A = big, b.lda = d.nhid, b.W = W(L.mlp2, L.mlp2_h, prec);
+    b.M = (int)R, b.N = E, b.K = d.nhid, b.X = X, b.ln_eps = d.ln_eps;
+    HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
+  }
+  return MMPFN_OK;
+}
+
+int decode(mmpfn_ctx* ctx, float* logits) {
+  const mmpfn_model_desc& d = ctx->d;
+  const int E = d.emsize, S = ctx->S, T = ctx->T, N = ctx->N;
+  const float* Xl = (const float*)ctx->ws_X.p + ((size_t)(T - 1) * S + N) * E;
+  HIPCHK(launch_decoder(Xl, S - N, (const float*)ctx->dec_w1.p, (const float*)ctx->dec_b1.p, d.nhid,
+                        (const float*)ctx->dec_w2.p, (const float*)ctx->dec_b2.p, d.n_out, logits, E, ctx->stream));
+  return MMPFN_OK;
+}
+
+int mixer(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int prec) {
+  const mmpfn_model_desc& d = ctx->d;
+  const int E = d.emsize, D = d.nhid;
+  const bool bf = prec == PREC_BF16;
+  const int eb = bf ? 2 : 4;
+  hipStream_t st = ctx->stream;
+  const int64_t rows = (int64_t)S * n_mod;
+  if (d.mixer_type == MMPFN_MIXER_MGM || d.mixer_type == MMPFN_MIXER_MGM_CAP) {
+    const int mg = d.mgm_heads, M = mg * n_mod;
+    RC(ensure(ctx, ctx->mx[0], (size_t)rows * D * eb));               // normalised image
+    RC(ensure(ctx, ctx->mx[1], (size_t)rows * mg * (D / 2) * eb));    // GLU output
+    const bool final_mgm = d.mixer_type == MMPFN_MIXER_MGM;
+    float* mtok = final_mgm ? tokens : nullptr;
+    if (!final_mgm) {
+      RC(ensure(ctx, ctx->mx[2], (size_t)S * M * E * 4));
+      mtok = (float*)ctx->mx[2].p;
+    }
+    HIPCHK(launch_layernorm_rows(image, rows, D, 1e-5f, ctx->mx[0].p, !bf, nullptr, nullptr, st));
+    GemmArgs a = gargs();
+    a.A = ctx->mx[0].p, a.lda = D, a.W = W(ctx->mgm_w1, ctx->mgm_w1_h, prec), a.bias = (const float*)ctx->mgm_b1.p;
+    a.M = (int)rows, a.N = mg * D, a.K = D, a.C = ctx->mx[1].p, a.ldc = (int64_t)mg * (D / 2);
+    HIPCHK(launch_gemm(a, prec, EPI_GLU, !bf, !bf, 1, st));
+    GemmArgs b = gargs();
+    b.A = ctx->mx[1].p, b.lda = (int64_t)mg * (D / 2), b.a_zstride = D / 2;
+    b.W = W(ctx->mgm_w2, ctx->mgm_w2_h, prec), b.w_zstride = (int64_t)E * (D / 2);
+    b.bias = (const float*)ctx->mgm_b2.p, b.b_zstride = E;
+    b.M = (int)rows, b.N = E, b.K = D / 2;
+    b.C = mtok, b.ldc = E, b.rdiv2 = n_mod, b.rmul2 = M, b.zmul = n_mod;
+    HIPCHK(launch_gemm(b, prec, EPI_REMAP, !bf, true, mg, st));
+    if (final_mgm) return MMPFN_OK;
+    // ---- CAP (transformer.py:77-88)
+    const int cap = d.cap_heads;
+    const int64_t srows = (int64_t)S * M;
+    RC(ensure(ctx, ctx->mx[3], (size_t)srows * E * eb));        // k_norm(src) (affine folded)
+    RC(ensure(ctx, ctx->mx[4], (size_t)srows * 2 * E * eb));    // K|V
+    RC(ensure(ctx, ctx->mx[5], (size_t)S * cap * E * 4));       // attention out (heads concat)
+    RC(ensure(ctx, ctx->mx[6], (size_t)S * cap * E * 4));       // out_proj
+    RC(ensure(ctx, ctx->mx[7], (size_t)S * cap * 2 * E * 4));   // ffn hidden (+ ffn out after)
+    HIPCHK(launch_layernorm_rows(mtok, srows, E, 1e-5f, ctx->mx[3].p, !bf, nullptr, nullptr, st));
+    GemmArgs c = gargs();
+    c.A = ctx->mx[3].p, c.lda = E, c.W = W(ctx->cap_kv, ctx->cap_kv_h, prec), c.bias = (const float*)ctx->cap_kv_b.p;
+    c.M = (int)srows, c.N = 2 * E, c.K = E, c.C = ctx->mx[4].p, c.ldc = 2 * E;
+    HIPCHK(launch_gemm(c, prec, EPI_STORE, !bf, !bf, 1, st));
+    HIPCHK(launch_cap_attention((const float*)ctx->cap_qp.p, ctx->mx[4].p, !bf, (float*)ctx->mx[5].p, S, M, cap, E,
+                                st));
+    const int64_t crow = (int64_t)S * cap;
+    // projections run in fp32 A (tiny); bf16 weights in perf mode
+    GemmArgs o = gargs();
+    o.A = ctx->mx[5].p, o.lda = E, o.W = W(ctx->cap_o, ctx->cap_o_h, prec), o.bias = (const float*)ctx->cap_o_b.p;
+    o.M = (int)crow, o.N = E, o.K = E, o.C = ctx->mx[6].p, o.ldc = E;
+    HIPCHK(launch_gemm(o, prec, EPI_STORE, true, true, 1, st));
+    GemmArgs f0 = gargs();
+    f0.A = ctx->mx[6].p, f0.lda = E, f0.W = W(ctx->cap_f0, ctx->cap_f0_h, prec);
+    f0.bias = (const float*)ctx->cap_f0_b.p, f0.act = ACT_GELU;
+    f0.M = (int)crow, f0.N = 2 * E, f0.K = E, f0.C = ctx->mx[7].p, f0.ldc = 2 * E;
+    HIPCHK(launch_gemm(f0, prec, EPI_STORE, true, true, 1, st));
+    GemmArgs f3 = gargs();
+    f3.A = ctx->mx[7].p, f3.lda = 2 * E, f3.W = W(ctx->cap_f3, ctx->cap_f3_h, prec);
+    f3.bias = (const float*)ctx->cap_f3_b.p;
+    f3.M = (int)crow, f3.N = E, f3.K = 2 * E, f3.C = ctx->mx[5].p, f3.ldc = E;  // reuse mx5 for ffn out
+    HIPCHK(launch_gemm(f3, prec, EPI_STORE, true, true, 1, st));
+    HIPCHK(launch_ln_add((const float*)ctx->mx[6].p, (const float*)ctx->mx[5].p, (const float*)ctx->cap_ng.p,
+                         (const float*)ctx->cap_nb.p, tokens, crow, E, 1e-5f, st));
+    return MMPFN_OK;
+  }
+  if (d.mixer_type == MMPFN_MIXER_MOE) {
+    const int ne = d.mgm_heads;
+    RC(ensure(ctx, ctx->mx[0], (size_t)S * D * eb));
+    RC(ensure(ctx, ctx->mx[1], (size_t)S * ne * (D / 2) * eb));
+    RC(ensure(ctx, ctx->mx[2], (size_t)S * ne * 4));
+    // modality 0 rows: image + s*n_mod*D  -> normalise with row stride n_mod*D
+    // (ln kernel assumes contiguous rows; handle stride by normalising all rows when n_mod==1,
+    //  else gather modality 0 first)
+    const float* x0 = image;
+    if (n_mod != 1) {
+      RC(ensure(ctx, ctx->mx[3], (size_t)S * D * 4));
+      HIPCHK(hipMemcpy2DAsync(ctx->mx[3].p, (size_t)D * 4, image, (size_t)n_mod * D * 4, (size_t)D * 4, S,
+                              hipMemcpyDeviceToDevice, st));
+      x0 = (const float*)ctx->mx[3].p;
+    }
+    HIPCHK(launch_layernorm_rows(x0, S, D, 1e-5f, ctx->mx[0].p, !bf, nullptr, nullptr, st));
+    GemmArgs a = gargs();
+    a.A = ctx->mx[0].p, a.lda = D, a.W = W(ctx->moe_w1, ctx->moe_w1_h, prec), a.bias = (const float*)ctx->moe_b1.p;
+    a.act = ACT_GELU, a.M = S, a.N = ne * (D / 2), a.K = D, a.C = ctx->mx[1].p, a.ldc = (int64_t)ne * (D / 2);
+    HIPCHK(launch_gemm(a, prec, EPI_STORE, !bf, !bf, 1, st));
+    GemmArgs b = gargs();
+    b.A = ctx->mx[1].p, b.lda = (int64_t)ne * (D / 2), b.a_zstride = D / 2;
+    b.W = W(ctx->moe_w2, ctx->moe_w2_h, prec), b.w_zstride = (int64_t)E * (D / 2);
+    b.bias = (const float*)ctx->moe_b2.p, b.b_zstride = E;
+    b.M = S, b.N = E, b.K = D / 2, b.C = tokens, b.ldc = E, b.rdiv2 = 1, b.rmul2 = ne, b.zmul = 1;
+    HIPCHK(launch_gemm(b, prec, EPI_REMAP, !bf, true, ne, st));
+    HIPCHK(launch_gate_softmax(x0, D, S, D, (const float*)ctx->moe_gw.p, (const float*)ctx->moe_gb.p, ne,
+                               (float*)ctx->mx[2].p, st));
+    HIPCHK(launch_scale_tokens(tokens, (const float*)ctx->mx[2].p, S, ne, E, st));
+    return MMPFN_OK;
+  }
+  return fail(ctx, MMPFN_ERR_INVALID, "model has no mixer");
+}
+
+}  // namespace
+
+// ===================================================================== C ABI
+extern "C" {
+
+const char* mmpfn_version(void) { return "mmpfn-hip 0.1 (gfx950)"; }
+
+mmpfn_ctx* mmpfn_create(int device, void* stream) {
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  mmpfn_ctx* c = new mmpfn_ctx();
+  c->device = device;
+  c->stream = (hipStream_t)stream;
+  return c;
+}
+
+void mmpfn_destroy(mmpfn_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  auto fr = [](DevBuf& b) {
+    if (b.p) hipFree(b.p);
+    b.p = nullptr;
+  };
+  for (auto& L : ctx->layers) {
+    for (DevBuf* b : {&L.feat_qkv, &L.feat_out, &L.item_qkv, &L.item_qtest, &L.item_out, &L.mlp1, &L.mlp2,
+                      &L.feat_qkv_h, &L.feat_out_h, &L.item_qkv_h, &L.item_qtest_h, &L.item_out_h, &L.mlp1_h,
+                      &L.mlp2_h})
+      fr(*b);
+  }
+  for (DevBuf* b : {&ctx->enc_w, &ctx->y_w, &ctx->y_b, &ctx->pe_w, &ctx->pe_b, &ctx->dec_w1, &ctx->dec_b1,
+                    &ctx->dec_w2, &ctx->dec_b2, &ctx->mgm_w1, &ctx->mgm_w1_h, &ctx->mgm_b1, &ctx->mgm_w2,
+                    &ctx->mgm_w2_h, &ctx->mgm_b2, &ctx->cap_qp, &ctx->cap_kv, &ctx->cap_kv_h, &ctx->cap_kv_b,
+                    &ctx->cap_o, &ctx->cap_o_h, &ctx->cap_o_b, &ctx->cap_f0, &ctx->cap_f0_h, &ctx->cap_f0_b,
+                    &ctx->cap_f3, &ctx->cap_f3_h, &ctx->cap_f3_b, &ctx->cap_ng, &ctx->cap_nb, &ctx->moe_w1,
+                    &ctx->moe_w1_h, &ctx->moe_b1, &ctx->moe_w2, &ctx->moe_w2_h, &ctx->moe_b2, &ctx->moe_gw,
+                    &ctx->moe_gb, &ctx->ws_X, &ctx->ws_O, &ctx->ws_big, &ctx->ws_pe, &ctx->ws_slots, &ctx->ws_scr,
+                    &ctx->ws_flag})
+    fr(*b);
+  for (auto& b : ctx->mx) fr(b);
+  delete ctx;
+}
+
+const char* mmpfn_last_error(const mmpfn_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int mmpfn_set_stream(mmpfn_ctx* ctx, void* stream) {
+  if (!ctx) return MMPFN_ERR_INVALID;
+  ctx->stream = (hipStream_t)stream;
+  return MMPFN_OK;
+}
+
+int mmpfn_set_model(mmpfn_ctx* ctx, const mmpfn_model_desc* desc) {
+  if (!ctx || !desc) return MMPFN_ERR_INVALID;
+  const mmpfn_model_desc& d = *desc;
+  if (d.emsize != 192 || d.nhead * 32 != d.emsize)
+    return fail(ctx, MMPFN_ERR_INVALID, "engine is specialised for emsize 192 with head dim 32");
+  if (d.nhid % 192 != 0 || d.nlayers <= 0 || d.features_per_group <= 0 || d.features_per_group > 8 ||
+      d.encoder_features < d.features_per_group || d.encoder_features > 8 || d.n_out <= 0)
+    return fail(ctx, MMPFN_ERR_INVALID, "unsupported model geometry");
+  if (d.mixer_type == MMPFN_MIXER_MGM_CAP && (d.cap_heads <= 0 || d.emsize % d.cap_heads != 0))
+    return fail(ctx, MMPFN_ERR_INVALID, "cap_heads must divide emsize");
+  ctx->d = d;
+  ctx->have_model = true;
+  ctx->finalized = false;
+  ctx->host.clear();
+  return MMPFN_OK;
+}
+
+int mmpfn_load_weight(mmpfn_ctx* ctx, const char* name, const float* data, int64_t numel) {
+  if (!ctx || !name || (!data && numel)) return MMPFN_ERR_INVALID;
+  if (!ctx->have_model) return fail(ctx, MMPFN_ERR_STATE, "mmpfn_set_model first");
+  ctx->host[name].assign(data, data + numel);
+  ctx->finalized = false;
+  return MMPFN_OK;
+}
+
+int mmpfn_finalize_weights(mmpfn_ctx* ctx) {
+  if (!ctx) return MMPFN_ERR_INVALID;
+  if (!ctx->have_model) return fail(ctx, MMPFN_ERR_STATE, "mmpfn_set_model first");
+  HIPCHK(hipSetDevice(ctx->device));
+  int rc = finalize(ctx);
+  if (rc == MMPFN_OK) {
+    ctx->finalized = true;
+    ctx->host.clear();
+  }
+  return rc;
+}
+
+int mmpfn_mixer_tokens(const mmpfn_ctx* ctx, int n_mod) {
+  if (!ctx) return MMPFN_ERR_INVALID;
+  switch (ctx->d.mixer_type) {
+    case MMPFN_MIXER_MGM: return ctx->d.mgm_heads * n_mod;
+    case MMPFN_MIXER_MGM_CAP: return ctx->d.cap_heads;
+    case MMPFN_MIXER_MOE: return ctx->d.mgm_heads;
+  }
+  return 0;
+}
+
+int mmpfn_mixer_forward(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int precision) {
+  if (!ctx || !image || !tokens || S <= 0 || n_mod <= 0) return MMPFN_ERR_INVALID;
+  if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
+  HIPCHK(hipSetDevice(ctx->device));
+  return mixer(ctx, image, S, n_mod, tokens, precision);
+}
+
+int mmpfn_embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int C, const float* y, int N,
+                const float* uniq, int U, const float* pos_rand, int precision) {
+  if (!ctx) return MMPFN_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  return embed(ctx, x, S, F, tokens, C, y, N, uniq, U, pos_rand, precision);
+}
+
+int mmpfn_run_layers(mmpfn_ctx* ctx, int l0, int l1) {
+  if (!ctx) return MMPFN_ERR_INVALID;
+  if (!ctx->embedded) return fail(ctx, MMPFN_ERR_STATE, "mmpfn_embed first");
+  if (l0 < 0 || l1 > ctx->d.nlayers || l0 > l1) return fail(ctx, MMPFN_ERR_INVALID, "bad layer range");
+  HIPCHK(hipSetDevice(ctx->device));
+  for (int l = l0; l < l1; ++l) RC(run_layer(ctx, l));
+  return MMPFN_OK;
+}
+
+int mmpfn_decode(mmpfn_ctx* ctx, float* logits) {
+  if (!ctx || !logits) return MMPFN_ERR_INVALID;
+  if (!ctx->embedded) return fail(ctx, MMPFN_ERR_STATE, "mmpfn_embed first");
+  HIPCHK(hipSetDevice(ctx->device));
+  return decode(ctx, logits);
+}
+
+int mmpfn_forward(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int C, const float* y, int N,
+                  const float* uniq, int U, const float* pos_rand, float* logits, int precision) {
+  if (!ctx || !logits) return MMPFN_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  RC(embed(ctx, x, S, F, tokens, C, y, N, uniq, U, pos_rand, precision));
+  for (int l = 0; l < ctx->d.nlayers; ++l) RC(run_layer(ctx, l));
+  return decode(ctx, logits);
+}
+
+int mmpfn_state_tokens(const mmpfn_ctx* ctx) { return ctx ? ctx->T : 0; }
+
+int mmpfn_copy_state(mmpfn_ctx* ctx, float* out, int64_t cap) {
+  if (!ctx || !out) return MMPFN_ERR_INVALID;
+  const int S = ctx->S, T = ctx->T, E = ctx->d.emsize;
+  if (cap < (int64_t)S * T * E) return fail(ctx, MMPFN_ERR_INVALID, "state buffer too small");
+  // [T][S][E] -> [S][T][E]
+  for (int t = 0; t < T; ++t)
+    HIPCHK(hipMemcpy2DAsync(out + (size_t)t * E, (size_t)T * E * 4, (const float*)ctx->ws_X.p + (size_t)t * S * E,
+                            (size_t)E * 4, (size_t)E * 4, S, hipMemcpyDeviceToDevice, ctx->stream));
+  return MMPFN_OK;
+}
+
+int mmpfn_status(mmpfn_ctx* ctx) {
+  if (!ctx) return MMPFN_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->ws_flag.p) {
+    int f = 0;
+    HIPCHK(hipMemcpy(&f, ctx->ws_flag.p, 4, hipMemcpyDeviceToHost));
+    if (f) return fail(ctx, MMPFN_ERR_NAN, "There should be no NaNs in the encoded x and y (flag " + std::to_string(f) + ")");
+  }
+  return MMPFN_OK;
+}
+
+int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
+                         int Npad, int s0, int nq, int nk, int kvh, int precision) {
+  if (!ctx || !q || !k || !vt || !out) return MMPFN_ERR_INVALID;
+  if (s0 < 0 || nq < 0 || s0 + nq > S || nk <= 0 || nk > Npad || Npad % 64 || H <= 0 || T <= 0 || kvh >= H)
+    return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(launch_attn_item(q, k, vt, out, S, T, H, Npad, s0, nq, nk, kvh, precision, ctx->stream));
+  return MMPFN_OK;
+}
+
+}  // extern "C"

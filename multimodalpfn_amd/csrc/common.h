@@ -1,0 +1,73 @@
+// Shared device helpers for the MMPFN gfx950 (CDNA4) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * wave = 64 lanes; all MFMA fragment maps are the gfx950 ones
+//    (cdna_hip_programming.md section 3):
+//      16x16x32 bf16 : lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15], j=0..7
+//      16x16x4  f32  : lane l holds A[l&15][l>>4],      B[l>>4][l&15]
+//      32x32x16 bf16 : lane l holds A[l&31][8(l>>5)+j], B[8(l>>5)+j][l&31]
+//      32x32x2  f32  : lane l holds A[l&31][l>>5],      B[l>>5][l&31]
+//      C/D 16x16     : col = l&15, row = 4(l>>4)+r            (r = 0..3)
+//      C/D 32x32     : col = l&31, row = (r&3)+8(r>>2)+4(l>>5) (r = 0..15)
+//  * "bf16" storage is the clang __bf16 type (RNE conversion, NaN preserving).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mmpfn {
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// exact GELU (torch default, approximate='none')
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide sum for 256-thread blocks (4 waves); `red` needs 4 slots
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  v = wave_sum_d(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  const int nw = (blockDim.x + 63) >> 6;
+  for (int i = 0; i < nw; ++i) r += red[i];
+  return r;
+}
+
+}  // namespace mmpfn

@@ -1,0 +1,350 @@
+// Input encoders, positional embedding, token assembly and decoder head (gfx950).
+//
+// x encoder (loading.py:308-371; encoders.py): one block per feature group computes
+// the column statistics the reference fits on the train rows -- constancy over ALL
+// rows (encoders.py:515), NaN/inf fill with the train nanmean (encoders.py:461-493),
+// the two-pass 12-sigma soft outlier bounds (encoders.py:133-162), train z-score
+// (encoders.py:53-99) and the used-feature rescale (encoders.py:608-655).  A second
+// kernel applies them element-wise, embeds with Linear(2*nf -> E) and adds the
+// subspace positional embedding (transformer.py:925-933), writing token g of the
+// [T][S][E] state.  Reductions accumulate in fp64.
+#include "common.h"
+#include "kernels.h"
+
+namespace mmpfn {
+
+namespace {
+
+__device__ __forceinline__ bool bad(float v) { return isnan(v) || isinf(v); }
+
+__device__ __forceinline__ float soft_clip(float v, float lo, float hi) {
+  v = fmaxf(-logf(1.0f + fabsf(v)) + lo, v);  // encoders.py:160
+  v = fminf(logf(1.0f + fabsf(v)) + hi, v);   // encoders.py:161
+  return v;
+}
+
+// NaN-propagating max/min matching torch.maximum / torch.minimum
+__device__ __forceinline__ float tmax(float a, float b) { return (isnan(a) || isnan(b)) ? NAN : fmaxf(a, b); }
+__device__ __forceinline__ float tmin(float a, float b) { return (isnan(a) || isnan(b)) ? NAN : fminf(a, b); }
+__device__ __forceinline__ float soft_clip_t(float v, float lo, float hi) {
+  v = tmax(-logf(1.0f + fabsf(v)) + lo, v);
+  v = tmin(logf(1.0f + fabsf(v)) + hi, v);
+  return v;
+}
+
+struct Moments {  // torch_nanmean (clipped count) and torch_nanstd (unbiased)
+  float mean_clip, std;
+};
+
+// nan-skipping moments of f(s) over rows [0, n); f returns NaN to skip
+template <typename Fn>
+__device__ Moments nan_moments(int n, Fn f, double* red) {
+  double sum = 0.0, cnt = 0.0;
+  for (int s = threadIdx.x; s < n; s += blockDim.x) {
+    const float v = f(s);
+    if (!isnan(v)) {
+      sum += (double)v;
+      cnt += 1.0;
+    }
+  }
+  sum = block_sum_d(sum, red);
+  cnt = block_sum_d(cnt, red + 4);
+  const double mu = sum / cnt;  // unclipped (torch_nanstd)
+  double ss = 0.0;
+  for (int s = threadIdx.x; s < n; s += blockDim.x) {
+    const float v = f(s);
+    if (!isnan(v)) {
+      const double dl = mu - (double)v;
+      ss += dl * dl;
+    }
+  }
+  ss = block_sum_d(ss, red + 8);
+  Moments m;
+  m.mean_clip = (float)(sum / (cnt < 1.0 ? 1.0 : cnt));
+  m.std = (float)sqrt(ss / (cnt - 1.0));
+  return m;
+}
+
+__global__ __launch_bounds__(256) void enc_x_stats_kernel(const float* __restrict__ x, int S, int F, int N, int fpg,
+                                                          int nf, float sigma, SlotParams* __restrict__ slots) {
+  __shared__ double red[16];
+  __shared__ int s_cnt[8];
+  const int g = blockIdx.x;
+  // 1. constancy over all rows (RemoveEmptyFeatures) for each column of the group
+  int src_of_slot[8];
+  int nsel = 0;
+  for (int j = 0; j < fpg; ++j) {
+    const int c = g * fpg + j;
+    int eq = 0;
+    if (c < F) {
+      const float x0 = x[c];
+      for (int s = 1 + threadIdx.x; s < S; s += blockDim.x) eq += (x[(int64_t)s * F + c] == x0);
+    } else {
+      for (int s = 1 + threadIdx.x; s < S; s += blockDim.x) eq += 1;  // zero padding column
+    }
+    const double tot = block_sum_d((double)eq, red);
+    const bool sel = (int)(tot + 0.5) != S - 1;
+    if (sel) src_of_slot[nsel++] = c;
+  }
+  for (int k = nsel; k < fpg; ++k) src_of_slot[k] = -1;
+
+  int used = 0;
+  SlotParams sp[8];
+  for (int k = 0; k < fpg; ++k) {
+    const int c = src_of_slot[k];
+    SlotParams p;
+    p.src = c;
+    p.fill = 0.f;
+    p.lo = -INFINITY;
+    p.hi = INFINITY;
+    p.mean = 0.f;
+    p.sd = 1.f;
+    p.scale = 1.f;
+    if (c >= 0) {
+      auto raw = [&](int s) { return x[(int64_t)s * F + c]; };
+      // NaN handling: torch.nanmean over train rows (inf included)
+      {
+        double sum = 0.0, cnt = 0.0;
+        for (int s = threadIdx.x; s < N; s += blockDim.x) {
+          const float v = raw(s);
+          if (!isnan(v)) {
+            sum += (double)v;
+            cnt += 1.0;
+          }
+        }
+        sum = block_sum_d(sum, red);
+        cnt = block_sum_d(cnt, red + 4);
+        p.fill = (float)(sum / cnt);
+      }
+      const float fill = p.fill;
+      auto filled = [&](int s) {
+        const float v = raw(s);
+        return bad(v) ? fill : v;
+      };
+      if (sigma > 0.f) {
+        const Moments a = nan_moments(N, filled, red);
+        const float lo1 = a.mean_clip - a.std * sigma, hi1 = a.mean_clip + a.std * sigma;
+        auto cleaned = [&](int s) {
+          const float v = filled(s);
+          return (v > hi1 || v < lo1) ? NAN : v;
+        };
+        const Moments b = nan_moments(N, cleaned, red);
+        p.lo = b.mean_clip - b.std * sigma;
+        p.hi = b.mean_clip + b.std * sigma;
+      }
+      const float lo = p.lo, hi = p.hi;
+      const bool clipping = sigma > 0.f;
+      auto clipped = [&](int s) {
+        const float v = filled(s);
+        return clipping ? soft_clip_t(v, lo, hi) : v;
+      };
+      const Moments nm = nan_moments(N, clipped, red);
+      p.mean = nm.mean_clip;
+      p.sd = (S == 1 || N == 1) ? 1.0f : nm.std + 1e-20f;
+      // used-feature test on the normalised values over all rows
+      const float mean = p.mean, sd = p.sd;
+      auto normed = [&](int s) { return tmin(tmax((clipped(s) - mean) / sd, -100.f), 100.f); };
+      const float u0 = normed(0);
+      int eq = 0;
+      for (int s = 1 + threadIdx.x; s < S; s += blockDim.x) eq += (normed(s) == u0);
+      const double tot = block_sum_d((double)eq, red);
+      if ((int)(tot + 0.5) != S - 1) ++used;
+    }
+    sp[k] = p;
+  }
+  (void)s_cnt;
+  const float scale = sqrtf((float)nf / (float)(used < 1 ? 1 : used));
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < fpg; ++k) {
+      sp[k].scale = scale;
+      slots[g * fpg + k] = sp[k];
+    }
+  }
+}
+
+// one thread per (token, 4 embedding columns)
+__global__ __launch_bounds__(256) void enc_x_embed_kernel(const float* __restrict__ x, int S, int F, int G, int fpg,
+                                                          int nf, const SlotParams* __restrict__ slots,
+                                                          const float* __restrict__ w, const float* __restrict__ pe,
+                                                          float* __restrict__ X, int E, int* flag) {
+  const int E4 = E / 4;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)S * G * E4) return;
+  const int e4 = idx % E4;
+  const int64_t tok = idx / E4;
+  const int s = tok % S, g = tok / S;
+  float u[8], ind[8];
+  for (int k = 0; k < nf; ++k) u[k] = ind[k] = 0.f;
+  for (int k = 0; k < fpg; ++k) {
+    const SlotParams p = slots[g * fpg + k];
+    if (p.src < 0) continue;
+    const float raw = x[(int64_t)s * F + p.src];
+    ind[k] = isnan(raw) ? -2.0f : (isinf(raw) ? (raw > 0 ? 2.0f : 4.0f) : 0.0f);
+    float v = bad(raw) ? p.fill : raw;
+    v = soft_clip_t(v, p.lo, p.hi);
+    v = tmin(tmax((v - p.mean) / p.sd, -100.f), 100.f);
+    u[k] = v * p.scale;
+  }
+  const int nin = 2 * nf;
+  f32x4 o;
+  bool nan_seen = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = e4 * 4 + i;
+    const float* wr = w + e * nin;
+    float a = 0.f;
+    for (int k = 0; k < nf; ++k) a = fmaf(u[k], wr[k], a);
+    for (int k = 0; k < nf; ++k) a = fmaf(ind[k], wr[nf + k], a);
+    a += pe[g * E + e];
+    o[i] = a;
+    nan_seen |= isnan(a);
+  }
+  *(f32x4*)(X + ((int64_t)g * S + s) * E + e4 * 4) = o;
+  if (nan_seen) atomicOr(flag, 1);
+}
+
+__global__ void y_stats_kernel(const float* __restrict__ y, int N, float* out) {
+  __shared__ double red[16];
+  double sum = 0.0, cnt = 0.0;
+  for (int s = threadIdx.x; s < N; s += blockDim.x) {
+    const float v = y[s];
+    if (!isnan(v)) {
+      sum += v;
+      cnt += 1.0;
+    }
+  }
+  sum = block_sum_d(sum, red);
+  cnt = block_sum_d(cnt, red + 4);
+  if (threadIdx.x == 0) out[0] = (float)(sum / cnt);
+}
+
+__global__ __launch_bounds__(256) void enc_y_embed_kernel(const float* __restrict__ y, int N, int S,
+                                                          const float* __restrict__ uniq, int U,
+                                                          const float* __restrict__ w, const float* __restrict__ b,
+                                                          const float* __restrict__ ymean, float* __restrict__ Xy,
+                                                          int E, int* flag) {
+  const int E4 = E / 4;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)S * E4) return;
+  const int e4 = idx % E4;
+  const int s = idx / E4;
+  float yv = s < N ? y[s] : NAN;
+  const float ind = isnan(yv) ? -2.0f : 0.0f;
+  if (isnan(yv)) yv = ymean[0];
+  float yc = 0.f;
+  for (int i = 0; i < U; ++i) yc += (yv > uniq[i]) ? 1.f : 0.f;
+  f32x4 o;
+  bool nan_seen = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = e4 * 4 + i;
+    const float a = fmaf(ind, w[e * 2 + 1], yc * w[e * 2]) + b[e];
+    o[i] = a;
+    nan_seen |= isnan(a);
+  }
+  *(f32x4*)(Xy + (int64_t)s * E + e4 * 4) = o;
+  if (nan_seen) atomicOr(flag, 2);
+}
+
+__global__ void pos_emb_kernel(const float* __restrict__ rnd, int n, const float* __restrict__ w,
+                               const float* __restrict__ b, float* __restrict__ out, int E) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * E) return;
+  const int e = idx % E, k = idx / E;
+  const int D = E / 4;
+  float a = 0.f;
+  for (int j = 0; j < D; ++j) a = fmaf(rnd[k * D + j], w[e * D + j], a);
+  out[idx] = a + b[e];
+}
+
+__global__ __launch_bounds__(256) void add_tokens_kernel(const float* __restrict__ tok, int S, int C,
+                                                         const float* __restrict__ pe, float* __restrict__ X, int E,
+                                                         int* flag) {
+  const int E4 = E / 4;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)S * C * E4) return;
+  const int e4 = idx % E4;
+  const int64_t r = idx / E4;  // r = c*S + s  (output order)
+  const int s = r % S, c = r / S;
+  f32x4 v = *(const f32x4*)(tok + ((int64_t)s * C + c) * E + e4 * 4);
+  const f32x4 p = *(const f32x4*)(pe + (int64_t)c * E + e4 * 4);
+  v += p;
+  *(f32x4*)(X + ((int64_t)c * S + s) * E + e4 * 4) = v;
+  if (isnan(v[0]) || isnan(v[1]) || isnan(v[2]) || isnan(v[3])) atomicOr(flag, 1);
+}
+
+// decoder: Linear(E, Fh) + GELU + Linear(Fh, n_out) on one query row per block
+__global__ __launch_bounds__(256) void decoder_kernel(const float* __restrict__ X, const float* __restrict__ w1,
+                                                      const float* __restrict__ b1, int Fh,
+                                                      const float* __restrict__ w2, const float* __restrict__ b2,
+                                                      int n_out, float* __restrict__ out, int E) {
+  extern __shared__ float sm[];
+  float* xs = sm;       // [E]
+  float* hs = sm + E;   // [Fh]
+  const int q = blockIdx.x;
+  for (int i = threadIdx.x; i < E; i += blockDim.x) xs[i] = X[(int64_t)q * E + i];
+  __syncthreads();
+  for (int o = threadIdx.x; o < Fh; o += blockDim.x) {
+    const float* wr = w1 + (int64_t)o * E;
+    float a = 0.f;
+    for (int k = 0; k < E; ++k) a = fmaf(xs[k], wr[k], a);
+    hs[o] = gelu_erf(a + b1[o]);
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int o = wave; o < n_out; o += blockDim.x / 64) {
+    const float* wr = w2 + (int64_t)o * Fh;
+    float a = 0.f;
+    for (int k = lane; k < Fh; k += 64) a = fmaf(hs[k], wr[k], a);
+    a = wave_sum(a);
+    if (lane == 0) out[(int64_t)q * n_out + o] = a + b2[o];
+  }
+}
+
+}  // namespace
+
+hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, int nf, float sigma,
+                           SlotParams* slots, const float* w_enc, const float* posemb, float* X, int E, int* flag,
+                           hipStream_t st) {
+  if (G <= 0) return hipSuccess;
+  if (fpg > 8 || nf > 8 || nf < fpg) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(enc_x_stats_kernel, dim3(G), dim3(256), 0, st, x, S, F, N, fpg, nf, sigma, slots);
+  const int64_t n = (int64_t)S * G * (E / 4);
+  hipLaunchKernelGGL(enc_x_embed_kernel, dim3((n + 255) / 256), dim3(256), 0, st, x, S, F, G, fpg, nf, slots, w_enc,
+                     posemb, X, E, flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode_y(const float* y_train, int N, int S, const float* uniq, int U, const float* w,
+                           const float* b, float* Xy, int E, float* scratch, int* flag, hipStream_t st) {
+  hipLaunchKernelGGL(y_stats_kernel, dim3(1), dim3(256), 0, st, y_train, N, scratch);
+  const int64_t n = (int64_t)S * (E / 4);
+  hipLaunchKernelGGL(enc_y_embed_kernel, dim3((n + 255) / 256), dim3(256), 0, st, y_train, N, S, uniq, U, w, b,
+                     scratch, Xy, E, flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_pos_emb(const float* rnd, int n, const float* w, const float* b, float* out, int E,
+                          hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pos_emb_kernel, dim3((n * E + 255) / 256), dim3(256), 0, st, rnd, n, w, b, out, E);
+  return hipGetLastError();
+}
+
+hipError_t launch_add_tokens(const float* tok, int S, int C, const float* posemb, float* X, int E, int* flag,
+                             hipStream_t st) {
+  if (C <= 0) return hipSuccess;
+  const int64_t n = (int64_t)S * C * (E / 4);
+  hipLaunchKernelGGL(add_tokens_kernel, dim3((n + 255) / 256), dim3(256), 0, st, tok, S, C, posemb, X, E, flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_decoder(const float* X, int Q, const float* w1, const float* b1, int Fh, const float* w2,
+                          const float* b2, int n_out, float* out, int E, hipStream_t st) {
+  if (Q <= 0) return hipSuccess;
+  hipLaunchKernelGGL(decoder_kernel, dim3(Q), dim3(256), (E + Fh) * sizeof(float), st, X, w1, b1, Fh, w2, b2, n_out,
+                     out, E);
+  return hipGetLastError();
+}
+
+}  // namespace mmpfn

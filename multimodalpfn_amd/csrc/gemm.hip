@@ -1,0 +1,324 @@
+// MFMA GEMM  C[M,N] = A[M,K] . W[N,K]^T  with fused epilogues, for gfx950.
+//
+// Used for every dense contraction of the PerFeatureTransformer forward:
+//   QKV projections (transformer.py / multi_head_attention.py:423-445),
+//   attention output projection + residual + LayerNorm (layer.py:437-455),
+//   MLP up (+GELU) and down (+residual+LN) (mlp.py:93-104),
+//   MGM / CAP / MoE projection heads (transformer.py:33-128).
+//
+// Tile: 64 (M) x 192 (N) per 256-thread block, 4 waves as 2 (M) x 2 (N), each wave
+// 32 x 96 = 2 x 6 MFMA tiles of 16 x 16.  K is staged through LDS in 128-byte row
+// slices (64 bf16 or 32 f32), with the next slice's global loads in flight while
+// the current one is consumed (register staging, issue-early / write-late).
+//   bf16 path : v_mfma_f32_16x16x32_bf16, fp32 accumulate
+//   f32  path : v_mfma_f32_16x16x4_f32 (exact fp32 fma chain; parity mode)
+// A may be stored fp32 while the bf16 path computes: it is converted when written
+// to LDS, so the fp32 residual stream is never materialised in bf16 in HBM.
+#include "common.h"
+#include "kernels.h"
+
+namespace mmpfn {
+
+namespace {
+
+constexpr int BM = 64;
+constexpr int BN = 192;
+constexpr int ROWB = 144;  // LDS bytes per staged row: 128 data + 16 pad (conflict-free b128 reads)
+constexpr int LDS_STAGE = (BM + BN) * ROWB;
+constexpr int LN_STRIDE = 196;  // floats per row of the LayerNorm epilogue buffer
+constexpr int LDS_LN = BM * LN_STRIDE * 4;
+constexpr int A_CHUNKS = BM * 8 / 256;  // 16-byte LDS chunks per thread
+constexpr int W_CHUNKS = BN * 8 / 256;
+
+template <bool BF16, bool AF32>
+struct Stage {
+  // raw staged A data per chunk: f32 source feeding bf16 compute needs 32 bytes
+  static constexpr int AWORDS = (BF16 && AF32) ? 2 : 1;
+};
+
+template <bool BF16, bool AF32, bool OF32, int EPI>
+__global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* As = smem;
+  unsigned char* Ws = smem + BM * ROWB;
+  typedef typename std::conditional<OF32, float, bf16>::type TO;
+  constexpr int EB = BF16 ? 2 : 4;       // compute element bytes
+  constexpr int BK = 128 / EB;           // K per staged slice
+  constexpr int AW = Stage<BF16, AF32>::AWORDS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int z = blockIdx.z;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int M = p.M, K = p.K;
+
+  const unsigned char* Abase = (const unsigned char*)p.A + (int64_t)z * p.a_zstride * (AF32 ? 4 : 2);
+  const unsigned char* Wbase = (const unsigned char*)p.W + (int64_t)z * p.w_zstride * EB;
+
+  // per-thread A row pointers (row -> memory row remap), computed once
+  const unsigned char* arow[A_CHUNKS];
+  int ach[A_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < A_CHUNKS; ++i) {
+    const int c = tid + 256 * i;
+    const int r = c >> 3;
+    ach[i] = c & 7;
+    const int64_t m = m0 + r;
+    if (m < M) {
+      const int64_t mr = (m / p.a_rdiv) * p.a_rmul + p.a_roff + (m % p.a_rdiv);
+      arow[i] = Abase + mr * p.lda * (AF32 ? 4 : 2);
+    } else {
+      arow[i] = nullptr;
+    }
+  }
+
+  u32x4 ra[A_CHUNKS][AW];
+  u32x4 rw[W_CHUNKS];
+
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_CHUNKS; ++i) {
+      if (arow[i]) {
+        if (BF16 && AF32) {
+          const float* src = (const float*)arow[i] + k0 + ach[i] * 8;
+          ra[i][0] = *(const u32x4*)src;
+          ra[i][AW - 1] = *(const u32x4*)(src + 4);
+        } else {
+          ra[i][0] = *(const u32x4*)(arow[i] + ((int64_t)k0 + ach[i] * (16 / EB)) * EB);
+        }
+      } else {
+#pragma unroll
+        for (int w = 0; w < AW; ++w) ra[i][w] = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < W_CHUNKS; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c >> 3, ch = c & 7;
+      rw[i] = *(const u32x4*)(Wbase + ((int64_t)(n0 + r) * K + k0 + ch * (16 / EB)) * EB);
+    }
+  };
+
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < A_CHUNKS; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c >> 3;
+      u32x4 v;
+      if (BF16 && AF32) {
+        const f32x4 f0 = __builtin_bit_cast(f32x4, ra[i][0]);
+        const f32x4 f1 = __builtin_bit_cast(f32x4, ra[i][AW - 1]);
+        bf16x8 b;
+        b[0] = (bf16)f0[0]; b[1] = (bf16)f0[1]; b[2] = (bf16)f0[2]; b[3] = (bf16)f0[3];
+        b[4] = (bf16)f1[0]; b[5] = (bf16)f1[1]; b[6] = (bf16)f1[2]; b[7] = (bf16)f1[3];
+        v = __builtin_bit_cast(u32x4, b);
+      } else {
+        v = ra[i][0];
+      }
+      *(u32x4*)(As + r * ROWB + ach[i] * 16) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < W_CHUNKS; ++i) {
+      const int c = tid + 256 * i;
+      *(u32x4*)(Ws + (c >> 3) * ROWB + (c & 7) * 16) = rw[i];
+    }
+  };
+
+  f32x4 acc[2][6];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  load_tile(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (kt + 1 < nk) load_tile((kt + 1) * BK);
+    const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if constexpr (BF16) {
+        bf16x8 af[2], bw[6];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          af[mt] = *(const bf16x8*)(As + (wm * 32 + mt * 16 + fr) * ROWB + ks * 64 + fg * 16);
+#pragma unroll
+        for (int nt = 0; nt < 6; ++nt)
+          bw[nt] = *(const bf16x8*)(Ws + (wn * 96 + nt * 16 + fr) * ROWB + ks * 64 + fg * 16);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 6; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bw[nt], acc[mt][nt], 0, 0, 0);
+      } else {
+        f32x4 af[2], bw[6];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          af[mt] = *(const f32x4*)(As + (wm * 32 + mt * 16 + fr) * ROWB + ks * 64 + fg * 16);
+#pragma unroll
+        for (int nt = 0; nt < 6; ++nt)
+          bw[nt] = *(const f32x4*)(Ws + (wn * 96 + nt * 16 + fr) * ROWB + ks * 64 + fg * 16);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 6; ++nt)
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mt][e], bw[nt][e], acc[mt][nt], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- epilogues
+  const int fr = lane & 15, fg = lane >> 4;
+  const float* bias = p.bias ? p.bias + (int64_t)z * p.b_zstride : nullptr;
+
+  if constexpr (EPI == EPI_RES_LN) {
+    float* Es = (float*)smem;
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 6; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rl = wm * 32 + mt * 16 + fg * 4 + r;
+          const int cl = wn * 96 + nt * 16 + fr;
+          const int64_t m = m0 + rl;
+          float v = acc[mt][nt][r] + (bias ? bias[cl] : 0.f);
+          if (m < M) v += p.X[m * 192 + cl];
+          Es[rl * LN_STRIDE + cl] = v;
+        }
+    __syncthreads();
+    const int row = tid >> 2, part = tid & 3;
+    const int64_t m = m0 + row;
+    const float* er = Es + row * LN_STRIDE + part * 48;
+    float s = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < 48; ++i) s += er[i];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    const float mean = s * (1.0f / 192.0f);
+    float q = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < 48; ++i) {
+      const float dlt = er[i] - mean;
+      q += dlt * dlt;
+    }
+    q += __shfl_xor(q, 1, 64);
+    q += __shfl_xor(q, 2, 64);
+    const float inv = 1.0f / sqrtf(q * (1.0f / 192.0f) + p.ln_eps);
+    if (m < M) {
+      float* xo = p.X + m * 192 + part * 48;
+#pragma unroll
+      for (int i = 0; i < 48; i += 4) {
+        f32x4 o;
+        o[0] = (er[i] - mean) * inv;
+        o[1] = (er[i + 1] - mean) * inv;
+        o[2] = (er[i + 2] - mean) * inv;
+        o[3] = (er[i + 3] - mean) * inv;
+        *(f32x4*)(xo + i) = o;
+      }
+    }
+    return;
+  } else if constexpr (EPI == EPI_GLU) {
+    TO* C = (TO*)p.C + (int64_t)z * p.c_zstride;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t m = m0 + wm * 32 + mt * 16 + fg * 4 + r;
+          if (m >= M) continue;
+          const int na = n0 + wn * 96 + q * 32 + fr;
+          float a = acc[mt][2 * q][r] + (bias ? bias[na] : 0.f);
+          float b = acc[mt][2 * q + 1][r] + (bias ? bias[na + 16] : 0.f);
+          const int64_t oc = (n0 + wn * 96) / 2 + q * 16 + fr;
+          C[m * p.ldc + oc] = from_f32<TO>(a * sigmoidf_(b));
+        }
+    return;
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 6; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t m = m0 + wm * 32 + mt * 16 + fg * 4 + r;
+          if (m >= M) continue;
+          const int n = n0 + wn * 96 + nt * 16 + fr;
+          float v = acc[mt][nt][r] + (bias ? bias[n] : 0.f);
+          if (p.act == ACT_GELU) v = gelu_erf(v);
+          if constexpr (EPI == EPI_STORE) {
+            TO* C = (TO*)p.C + (int64_t)z * p.c_zstride;
+            C[m * p.ldc + n] = from_f32<TO>(v);
+          } else if constexpr (EPI == EPI_REMAP) {
+            TO* C = (TO*)p.C;
+            const int64_t dr = (m / p.rdiv2) * p.rmul2 + (int64_t)z * p.zmul + (m % p.rdiv2);
+            C[dr * p.ldc + n] = from_f32<TO>(v);
+          } else if constexpr (EPI == EPI_ITEM_QKV) {
+            const int64_t t = m / p.a_rdiv, s = p.a_roff + m % p.a_rdiv;
+            const int E = p.H * 32;
+            const int j = n / E, h = (n % E) >> 5, d = n & 31;
+            const int64_t th = t * p.H + h;
+            if (j == 0)
+              ((TO*)p.q)[(th * p.S + s) * 32 + d] = from_f32<TO>(v);
+            else if (j == 1)
+              ((TO*)p.k)[(th * p.Npad + s) * 32 + d] = from_f32<TO>(v);
+            else
+              ((TO*)p.v)[(th * 32 + d) * p.Npad + s] = from_f32<TO>(v);
+          } else if constexpr (EPI == EPI_FEAT_QKV) {
+            const int64_t t = m / p.a_rdiv, s = m % p.a_rdiv;
+            const int E = p.H * 32;
+            const int j = n / E, h = (n % E) >> 5, d = n & 31;
+            ((TO*)p.q)[(((s * 3 + j) * p.H + h) * p.T + t) * 32 + d] = from_f32<TO>(v);
+          }
+        }
+  }
+}
+
+template <bool BF16, bool AF32, bool OF32, int EPI>
+hipError_t launch_t(const GemmArgs& a, int groups, hipStream_t st) {
+  dim3 grid((a.M + BM - 1) / BM, a.N / BN, groups);
+  const int lds = EPI == EPI_RES_LN ? (LDS_LN > LDS_STAGE ? LDS_LN : LDS_STAGE) : LDS_STAGE;
+  hipLaunchKernelGGL((gemm_kernel<BF16, AF32, OF32, EPI>), grid, dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+template <bool BF16, bool AF32, bool OF32>
+hipError_t launch_e(const GemmArgs& a, int epi, int groups, hipStream_t st) {
+  switch (epi) {
+    case EPI_STORE: return launch_t<BF16, AF32, OF32, EPI_STORE>(a, groups, st);
+    case EPI_ITEM_QKV: return launch_t<BF16, AF32, OF32, EPI_ITEM_QKV>(a, groups, st);
+    case EPI_FEAT_QKV: return launch_t<BF16, AF32, OF32, EPI_FEAT_QKV>(a, groups, st);
+    case EPI_RES_LN: return launch_t<BF16, AF32, true, EPI_RES_LN>(a, groups, st);
+    case EPI_GLU: return launch_t<BF16, AF32, OF32, EPI_GLU>(a, groups, st);
+    case EPI_REMAP: return launch_t<BF16, AF32, OF32, EPI_REMAP>(a, groups, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool out_f32, int groups,
+                       hipStream_t st) {
+  if (a.M <= 0) return hipSuccess;
+  if (a.N % BN != 0) return hipErrorInvalidValue;
+  if (prec == PREC_F32) {
+    if (!a_f32 || !out_f32) return hipErrorInvalidValue;
+    if (a.K % 32 != 0) return hipErrorInvalidValue;
+    return launch_e<false, true, true>(a, epi, groups, st);
+  }
+  if (a.K % 64 != 0) return hipErrorInvalidValue;
+  if (a_f32) {
+    return out_f32 ? launch_e<true, true, true>(a, epi, groups, st) : launch_e<true, true, false>(a, epi, groups, st);
+  }
+  return out_f32 ? launch_e<true, false, true>(a, epi, groups, st) : launch_e<true, false, false>(a, epi, groups, st);
+}
+
+}  // namespace mmpfn

@@ -1,0 +1,93 @@
+// Internal launch interface of the MMPFN HIP kernels (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mmpfn {
+
+enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1 };
+
+enum Epi : int {
+  EPI_STORE = 0,      // C[row] = act(acc + bias)
+  EPI_ITEM_QKV = 1,   // scatter to item-attention Q / K / V^T layouts
+  EPI_FEAT_QKV = 2,   // scatter to feature-attention [S][3][H][T][d] layout
+  EPI_RES_LN = 3,     // X[row] = LayerNorm(X[row] + acc), N == 192 (no affine)
+  EPI_GLU = 4,        // paired tiles: out = a * sigmoid(b) (weights row-interleaved)
+  EPI_REMAP = 5,      // grouped: dest row = (m / rdiv2) * rmul2 + z * zmul + m % rdiv2
+};
+
+enum Act : int { ACT_NONE = 0, ACT_GELU = 1 };
+
+struct GemmArgs {
+  // A: logical row m -> memory row (m / a_rdiv) * a_rmul + a_roff + (m % a_rdiv)
+  const void* A;
+  int64_t lda;
+  int64_t a_rdiv, a_rmul, a_roff;
+  int64_t a_zstride;  // elements between groups (blockIdx.z)
+  const void* W;      // [N][K] compute dtype, row-major
+  int64_t w_zstride;
+  const float* bias;  // [N] or null
+  int64_t b_zstride;
+  int M, N, K;
+  int act;
+  // plain / remap / glu output
+  void* C;
+  int64_t ldc;
+  int64_t c_zstride;
+  int64_t rdiv2, rmul2, zmul;
+  // attention scatter
+  void* q;  // Q  [T][H][S][d]          (item) | QKV [S][3][H][T][d] (feat)
+  void* k;  // K  [T][H][Npad][d]
+  void* v;  // V^T[T][H][d][Npad]
+  int S, Npad, T, H;
+  // LN epilogue
+  float* X;  // residual in / normalised out, ld = 192
+  float ln_eps;
+};
+
+// Launch C = A . W^T with the given epilogue.  `a_f32` says whether A is stored
+// as fp32 (otherwise bf16); `out_f32` likewise for C / scatter targets.
+hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool out_f32, int groups,
+                       hipStream_t st);
+
+// ---- attention -------------------------------------------------------------------
+// feature attention: qkv [S][3][H][T][d], out O [T][S][H*d]
+hipError_t launch_attn_feature(const void* qkv, void* out, int S, int T, int H, int prec, hipStream_t st);
+// item attention: queries s in [s0, s0+nq), keys [0, nk); kv_head_fixed >= 0 forces that KV head
+hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
+                            int Npad, int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st);
+
+// ---- encoders / decoder ------------------------------------------------------------
+struct SlotParams {  // per (group, slot): how to transform raw column -> model input
+  int src;           // source column or -1 (zero fill)
+  float fill;        // NaN/inf replacement (train nanmean)
+  float lo, hi;      // soft outlier bounds (or -inf/+inf when disabled)
+  float mean, sd;    // train z-score (sd already includes the +1e-20)
+  float scale;       // sqrt(nf / used) for the group
+};
+hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, int nf, float sigma,
+                           SlotParams* slots, const float* w_enc /*[E][2nf]*/, const float* posemb,
+                           float* X /*[T][S][E]*/, int E, int* flag, hipStream_t st);
+hipError_t launch_encode_y(const float* y_train, int N, int S, const float* uniq, int U,
+                           const float* w /*[E][2]*/, const float* b, float* Xy /*[S][E]*/, int E,
+                           float* scratch, int* flag, hipStream_t st);
+hipError_t launch_pos_emb(const float* rnd /*[n][E/4]*/, int n, const float* w /*[E][E/4]*/,
+                          const float* b, float* out /*[n][E]*/, int E, hipStream_t st);
+hipError_t launch_add_tokens(const float* tok /*[S][C][E]*/, int S, int C, const float* posemb /*[C][E]*/,
+                             float* X /*[C][S][E] slice*/, int E, int* flag, hipStream_t st);
+hipError_t launch_decoder(const float* X /*[Q][E]*/, int Q, const float* w1, const float* b1, int Fh,
+                          const float* w2, const float* b2, int n_out, float* out, int E, hipStream_t st);
+
+// ---- mixer helpers -----------------------------------------------------------------
+hipError_t launch_layernorm_rows(const float* in, int64_t rows, int dim, float eps, void* out, bool out_f32,
+                                 const float* gamma, const float* beta, hipStream_t st);
+hipError_t launch_cap_attention(const float* qp /*[cap][E]*/, const void* kv /*[S][M][2E]*/, bool kv_f32,
+                                float* out /*[S][cap][E]*/, int S, int M, int cap, int E, hipStream_t st);
+hipError_t launch_ln_add(const float* o, const float* f, const float* g, const float* b, float* out,
+                         int64_t rows, int E, float eps, hipStream_t st);
+hipError_t launch_gate_softmax(const float* x /*[S][D]*/, int64_t ldx, int S, int D, const float* w /*[n][D]*/,
+                               const float* b, int n, float* probs, hipStream_t st);
+hipError_t launch_scale_tokens(float* tok /*[S][n][E]*/, const float* probs /*[S][n]*/, int S, int n, int E,
+                               hipStream_t st);
+
+}  // namespace mmpfn

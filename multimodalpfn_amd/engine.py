@@ -1,0 +1,217 @@
+"""Host-side handle on one HIP engine context (one per GPU / rank).
+
+Owns the packed device weights (uploaded once through the checkpoint ABI) and
+drives the C-ABI entry points on the caller's current HIP stream.  All compute
+of the forward runs in ``libmmpfn_hip.so``; this module only moves pointers,
+shapes and the few host-side constants the reference also computes on the host:
+
+* the subspace positional-embedding draw ``torch.randn`` from the model's CPU
+  generator (``transformer.py:421-424,925-931``) -- a bit-exact RNG stream;
+* the sorted unique train labels of the target encoder (``encoders.py:956-958``).
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from multimodalpfn_amd import _lib
+from multimodalpfn_amd.model.spec import ModelConfig, encoder_linear_name
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def model_desc(cfg: ModelConfig) -> _lib.ModelDesc:
+    d = _lib.ModelDesc()
+    d.emsize = cfg.emsize
+    d.nhead = cfg.nhead
+    d.nlayers = cfg.nlayers
+    d.nhid = cfg.nhid
+    d.features_per_group = cfg.features_per_group
+    d.encoder_features = cfg.encoder_features
+    d.n_out = cfg.n_out
+    d.mixer_type = _lib.MIXER_CODES[cfg.mixer_type]
+    d.mgm_heads = cfg.mgm_heads
+    d.cap_heads = cfg.cap_heads
+    d.two_sets_of_queries = int(cfg.two_sets_of_queries)
+    d.remove_duplicate_features = int(cfg.remove_duplicate_features)
+    d.ln_eps = cfg.ln_eps
+    d.outlier_sigma = float(cfg.remove_outliers_sigma) if cfg.remove_outliers_sigma else 0.0
+    return d
+
+
+def pos_rand(cfg: ModelConfig, n_tokens: int) -> torch.Tensor:
+    """``randn((n_tokens, E//4))`` from a fresh CPU generator, seeded like the reference."""
+    gen = torch.Generator(device="cpu")
+    if cfg.model_seed:  # `if self.seed:` (transformer.py:423)
+        gen.manual_seed(cfg.model_seed)
+    return torch.randn((n_tokens, cfg.emsize // 4), generator=gen, dtype=torch.float32)
+
+
+def target_uniques(y_train: np.ndarray) -> np.ndarray:
+    """Sorted unique train targets after the y NaN fill (encoders.py:461-493,954-958)."""
+    y = np.asarray(y_train, dtype=np.float32)
+    if np.isnan(y).any():
+        y = np.where(np.isnan(y), np.float32(np.nanmean(y)), y)
+    return np.unique(y).astype(np.float32)
+
+
+class HipEngine:
+    """One ``mmpfn_ctx`` bound to a CUDA(HIP) device."""
+
+    def __init__(self, cfg: ModelConfig, state_dict: dict, device: torch.device):
+        if not torch.cuda.is_available():
+            raise RuntimeError("the MMPFN HIP engine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.lib = _lib.load_library()
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError(f"HipEngine needs a cuda device, got {self.device}")
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        self.ctx = self.lib.mmpfn_create(idx, ctypes.c_void_p(self._stream()))
+        if not self.ctx:
+            raise _lib.EngineError(f"mmpfn_create failed on device {idx}")
+        self.desc = model_desc(cfg)
+        self._check(self.lib.mmpfn_set_model(self.ctx, ctypes.byref(self.desc)), "mmpfn_set_model")
+        names = set()
+        for name, t in state_dict.items():
+            if isinstance(t, torch.Tensor):
+                a = t.detach().to("cpu", torch.float32).contiguous().numpy()
+            else:
+                a = np.ascontiguousarray(t, dtype=np.float32)
+            self._check(
+                self.lib.mmpfn_load_weight(self.ctx, name.encode(), a.ctypes.data_as(ctypes.c_void_p), a.size),
+                f"mmpfn_load_weight({name})",
+            )
+            names.add(name)
+        if encoder_linear_name(cfg) not in names:
+            raise _lib.EngineError(f"state_dict lacks {encoder_linear_name(cfg)}")
+        self._check(self.lib.mmpfn_finalize_weights(self.ctx), "mmpfn_finalize_weights")
+        self._pos_cache: dict[int, torch.Tensor] = {}
+
+    # ------------------------------------------------------------------ plumbing
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _check(self, rc: int, what: str) -> None:
+        _lib.check(self.lib, self.ctx, rc, what)
+
+    def _bind_stream(self) -> None:
+        self._check(self.lib.mmpfn_set_stream(self.ctx, ctypes.c_void_p(self._stream())), "mmpfn_set_stream")
+
+    def close(self) -> None:
+        if getattr(self, "ctx", None):
+            self.lib.mmpfn_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    def _dev(self, t, dtype=torch.float32) -> torch.Tensor:
+        if not isinstance(t, torch.Tensor):
+            t = torch.as_tensor(np.asarray(t))
+        return t.to(self.device, dtype).contiguous()
+
+    def _pos(self, n: int) -> torch.Tensor:
+        if n not in self._pos_cache:
+            self._pos_cache[n] = pos_rand(self.cfg, n).to(self.device)
+        return self._pos_cache[n]
+
+    # ------------------------------------------------------------------ compute
+    def mixer_tokens(self, image, precision: int) -> torch.Tensor:
+        """Modality projection heads: ``[S, n_mod, D]`` -> ``[S, C, E]`` tokens."""
+        img = self._dev(image)
+        if img.dim() == 2:
+            img = img.unsqueeze(1)
+        S, n_mod, D = img.shape
+        if D != self.cfg.mixer_in_dim:
+            raise ValueError(f"image embedding width {D} != {self.cfg.mixer_in_dim}")
+        C = self.lib.mmpfn_mixer_tokens(self.ctx, n_mod)
+        out = torch.empty((S, C, self.cfg.emsize), device=self.device, dtype=torch.float32)
+        self._bind_stream()
+        self._check(
+            self.lib.mmpfn_mixer_forward(self.ctx, _ptr(img), S, n_mod, _ptr(out), precision), "mmpfn_mixer_forward"
+        )
+        return out
+
+    def _prepare(self, x, tokens, y_train):
+        y_np = y_train.detach().float().cpu().numpy() if isinstance(y_train, torch.Tensor) else np.asarray(y_train)
+        y_np = y_np.reshape(-1).astype(np.float32)
+        N = y_np.shape[0]
+        xd = None if x is None else self._dev(x)
+        if xd is not None and xd.dim() == 3:  # [S, 1, F] seam layout
+            xd = xd.reshape(xd.shape[0], xd.shape[-1])
+        td = None if tokens is None else self._dev(tokens)
+        S = xd.shape[0] if xd is not None else td.shape[0]
+        F = xd.shape[1] if xd is not None else 0
+        C = td.shape[1] if td is not None else 0
+        if td is not None and td.shape[0] != S:
+            raise ValueError(f"tokens rows {td.shape[0]} != table rows {S}")
+        fpg = self.cfg.features_per_group
+        G = (F + fpg - 1) // fpg if xd is not None else 0
+        uniq = torch.from_numpy(target_uniques(y_np)).to(self.device)
+        yd = torch.from_numpy(y_np).to(self.device)
+        return xd, td, yd, uniq, S, F, C, N, G
+
+    def forward(self, x, tokens, y_train, precision: int, check_nan: bool = True) -> torch.Tensor:
+        """One ensemble member: logits ``[S - N, n_out]`` (fp32, on the engine device)."""
+        xd, td, yd, uniq, S, F, C, N, G = self._prepare(x, tokens, y_train)
+        if N < 1 or N > S:
+            raise ValueError(f"single_eval_pos must be in [1, {S}], got {N}")
+        pr = self._pos(G + C)
+        out = torch.empty((S - N, self.cfg.n_out), device=self.device, dtype=torch.float32)
+        self._bind_stream()
+        self._check(
+            self.lib.mmpfn_forward(
+                self.ctx, _ptr(xd), S, F, _ptr(td), C, _ptr(yd), N, _ptr(uniq), uniq.numel(), _ptr(pr), _ptr(out),
+                precision,
+            ),
+            "mmpfn_forward",
+        )
+        if check_nan:
+            self.status()
+        return out
+
+    def status(self) -> None:
+        self._check(self.lib.mmpfn_status(self.ctx), "mmpfn_forward")
+
+    # ------------------------------------------------------------------ parity taps
+    def embed_state(self, x, tokens, y_train, precision: int) -> torch.Tensor:
+        """Embedded transformer input in reference order ``[S, T, E]``."""
+        xd, td, yd, uniq, S, F, C, N, G = self._prepare(x, tokens, y_train)
+        pr = self._pos(G + C)
+        self._S = S
+        self._bind_stream()
+        self._check(
+            self.lib.mmpfn_embed(
+                self.ctx, _ptr(xd), S, F, _ptr(td), C, _ptr(yd), N, _ptr(uniq), uniq.numel(), _ptr(pr), precision
+            ),
+            "mmpfn_embed",
+        )
+        return self.copy_state()
+
+    def run_layers(self, l0: int, l1: int) -> torch.Tensor:
+        self._bind_stream()
+        self._check(self.lib.mmpfn_run_layers(self.ctx, l0, l1), "mmpfn_run_layers")
+        return self.copy_state()
+
+    def copy_state(self) -> torch.Tensor:
+        T = self.lib.mmpfn_state_tokens(self.ctx)
+        out = torch.empty((self._S, T, self.cfg.emsize), device=self.device, dtype=torch.float32)
+        self._check(self.lib.mmpfn_copy_state(self.ctx, _ptr(out), out.numel()), "mmpfn_copy_state")
+        torch.cuda.current_stream(self.device).synchronize()
+        return out
+
+    def decode(self, n_query: int) -> torch.Tensor:
+        out = torch.empty((n_query, self.cfg.n_out), device=self.device, dtype=torch.float32)
+        self._bind_stream()
+        self._check(self.lib.mmpfn_decode(self.ctx, _ptr(out)), "mmpfn_decode")
+        return out

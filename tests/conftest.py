@@ -1,0 +1,31 @@
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests" / "golden"))
+sys.path.insert(0, str(ROOT / "tests"))
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (ROCm GPU) and the built HIP library")
+    config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+def pytest_collection_modifyitems(config, items):
+    try:
+        import torch
+
+        has_gpu = torch.cuda.is_available()
+    except Exception:  # noqa: BLE001
+        has_gpu = False
+    if has_gpu:
+        return
+    skip = pytest.mark.skip(reason="no ROCm GPU visible")
+    for item in items:
+        if "gpu" in item.keywords:
+            item.add_marker(skip)
