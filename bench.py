@@ -1,0 +1,252 @@
+"""Headline benchmark: in-context rows/sec on PAD-UFES-20-shaped inputs (BASELINE.json).
+
+Workload (config C): N = 1838 support + Q = 460 query rows, F = 21
+features (18 categorical + 3 numeric), one 768-d image embedding per row, MGM (64
+heads) + CAP (24 queries) mixer, 12-layer E=192 PerFeatureTransformer, 4 ensemble
+members per GPU (feature-shuffle + class-permutation members as EnsembleConfig
+builds them), synthetic data and random-init weights of that architecture.
+
+One step = one ``predict_proba`` pass of the hot path with inputs resident in HBM:
+mixer once (the image is identical for every member), 4 member forwards per GPU,
+one RCCL all-gather of the per-member logits, ensemble softmax-mean.  ``value`` =
+sum over members of (N + Q) / wall time, aggregated over all ranks (weak scaling:
+4 members per GPU).  Launch with ``torchrun --nproc-per-node N bench.py --gpus N``
+for N > 1.
+
+Also reported: ``roofline`` of the dominant kernel (sample-axis attention, bf16
+MFMA; algorithmic flops 4*T*Nq*Nk*E per launch timed with HIP events on the
+engine stream) and ``cpu_baseline`` (the oracle's CPU restatement of the same
+forward -- the reference's torch-SDPA branch -- on the host cores, bounded sample).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests" / "golden"))
+
+METRIC = "in-context rows/sec (support+query), PAD-UFES-20 shape, 1/2/4/8 MI355X"
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+S_ROWS, N_TRAIN, N_FEAT, N_CAT, N_CLASSES = 2298, 1838, 21, 18, 6
+MGM, CAP, MEMBERS_PER_GPU = 64, 24, 4
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
+    p.add_argument("--members", type=int, default=MEMBERS_PER_GPU, help="members per GPU")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--attn-reps", type=int, default=20)
+    return p.parse_args()
+
+
+def build_workload(device, world, members_per_gpu):
+    from synth import synth_image, synth_labels, synth_state_dict, synth_table
+
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+    from multimodalpfn_amd.model.transformer import PerFeatureTransformer
+
+    cfg = ModelConfig(mgm_heads=MGM, cap_heads=CAP)
+    sd = synth_state_dict(state_dict_spec(cfg), 2)
+    model = PerFeatureTransformer(cfg)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    norm = next(e for e in model.encoder if "InputNormalizationEncoderStep" in str(e.__class__))
+    norm.remove_outliers, norm.remove_outliers_sigma = True, 12.0  # classifier.fit (classifier.py:396-406)
+    model.to(device)
+    x = synth_table(S_ROWS, N_FEAT, 2, n_cat=N_CAT)
+    y = synth_labels(S_ROWS, N_CLASSES, 2)
+    image = synth_image(S_ROWS, 1, 2)
+    M = members_per_gpu * world
+    rng = np.random.default_rng(0)
+    members = []
+    for m in range(M):
+        fperm = rng.permutation(N_FEAT)  # ShuffleFeaturesStep
+        cperm = rng.permutation(N_CLASSES)  # class_permutation
+        xm = torch.from_numpy(np.ascontiguousarray(x[:, fperm])).to(device)
+        ym = cperm[y[:N_TRAIN].astype(np.int64)].astype(np.float32)
+        members.append((xm, ym, np.argsort(cperm)))
+    return cfg, sd, model, x, y, image, members
+
+
+def time_item_attention(eng, T, reps):
+    """Average launch duration of the sample-axis attention kernel at the workload's shape."""
+    from multimodalpfn_amd import _lib
+
+    H, d, S, N = 6, 32, S_ROWS, N_TRAIN
+    Q = S - N
+    Npad = (N + 63) // 64 * 64
+    dev = eng.device
+    g = torch.Generator(device="cpu").manual_seed(0)
+    q = torch.randn(T, H, S, d, generator=g).to(dev, torch.bfloat16)
+    k = torch.randn(T, H, Npad, d, generator=g).to(dev, torch.bfloat16)
+    vt = torch.randn(T, H, d, Npad, generator=g).to(dev, torch.bfloat16)
+    o = torch.empty(T, S, H * d, device=dev, dtype=torch.bfloat16)
+    lib, ctx = eng.lib, eng.ctx
+    eng._bind_stream()
+    stream = torch.cuda.current_stream(dev)
+
+    def launch(s0, nq, kvh):
+        rc = lib.mmpfn_item_attention(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), S, T, H, Npad,
+                                      s0, nq, N, kvh, _lib.PREC_BF16)
+        assert rc == 0, lib.mmpfn_last_error(ctx)
+
+    res = {}
+    for name, (s0, nq, kvh, nqk) in {"train": (0, N, -1, N), "test": (N, Q, 0, Q)}.items():
+        for _ in range(3):
+            launch(s0, nq, kvh)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            launch(s0, nq, kvh)
+        e1.record(stream)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        flops = 4.0 * T * nqk * N * H * d
+        res[name] = (ms, flops)
+    ms_avg = (res["train"][0] + res["test"][0]) / 2
+    fl_avg = (res["train"][1] + res["test"][1]) / 2
+    achieved = fl_avg / (ms_avg * 1e-3) / 1e12
+    return {
+        "bound": "mfma",
+        "achieved": round(achieved, 1),
+        "peak": BF16_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
+        "traffic": None,
+        "kernel": "attn_item_kernel<bf16> (sample-axis attention)",
+        "per_launch_ms": {"train_rows": round(res["train"][0], 4), "test_rows_mqa": round(res["test"][0], 4)},
+        "per_launch_flop": {"train_rows": res["train"][1], "test_rows_mqa": res["test"][1]},
+    }
+
+
+def cpu_baseline(sd, x, y, image):
+    """Oracle (CPU restatement of the reference forward, SDPA branch) on one member."""
+    from multimodalpfn_amd.model.spec import ModelConfig
+    from oracle.forward import OracleSpec, oracle_forward
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = ModelConfig(mgm_heads=MGM, cap_heads=CAP)
+    spec = OracleSpec(mgm_heads=cfg.mgm_heads, cap_heads=cfg.cap_heads)
+    w = {k: torch.from_numpy(v) for k, v in sd.items()}
+    args = (spec, w, torch.from_numpy(x), torch.from_numpy(image), torch.from_numpy(y[:N_TRAIN]))
+    t0 = time.perf_counter()
+    oracle_forward(*args, use_sdpa=True)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(S_ROWS / dt, 2),
+        "unit": "rows/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"1 member forward of config C (S={S_ROWS}, 12 layers, MGM64+CAP24, fp32, torch SDPA "
+                  f"branch) on {threads} host threads: {dt:.1f} s",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from multimodalpfn_amd import _lib
+    from multimodalpfn_amd.parallel import allgather_logits, lpt_assign
+
+    prec = _lib.PREC_BF16 if args.precision == "bf16" else _lib.PREC_F32
+    cfg, sd, model, x, y, image, members = build_workload(device, world, args.members)
+    eng = model.engine(device)
+    img = torch.from_numpy(image).to(device)
+    M = len(members)
+    T = (N_FEAT + 1) // 2 + CAP + 1
+    assignment = lpt_assign([float(T * S_ROWS * N_TRAIN)] * M, world)
+    mine = assignment[rank]
+    perms = np.stack([members[m][2] for m in range(M)])
+
+    def step():
+        tokens = eng.mixer_tokens(img, prec)
+        outs = [eng.forward(members[m][0], tokens, members[m][1], prec, check_nan=False) for m in mine]
+        local = torch.stack(outs)
+        allm = allgather_logits(local, assignment, rank)
+        return eng.aggregate(allm, perms, N_CLASSES, 0.9, False)
+
+    probs = step()
+    eng.status()  # NaN check once (reference raises ValueError)
+    assert torch.isfinite(probs).all()
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    rows = M * S_ROWS * args.steps
+    value = rows / dt
+
+    roof = time_item_attention(eng, T, args.attn_reps) if rank == 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(sd, x, y, image)
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if prec == _lib.PREC_BF16 else "f32",
+            "data": "synthetic (PAD-UFES-20 shape; random-init weights of the MMPFN architecture)",
+            "config": {
+                "workload": "config C: PAD-UFES-20 image+tabular, N=1838 support + Q=460 query rows, F=21 "
+                            "(18 cat + 3 num), image [S,1,768], MGM 64 heads + CAP 24, 12 layers E=192",
+                "members_per_gpu": args.members,
+                "members_total": M,
+                "rows_per_member": S_ROWS,
+                "tokens_per_row": T,
+                "parallelism": f"ensemble members sharded over {world} GPU(s) + RCCL all-gather of logits",
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -104,6 +104,14 @@ int mmpfn_decode(mmpfn_ctx* ctx, float* logits);
 int mmpfn_copy_state(mmpfn_ctx* ctx, float* out, int64_t capacity_elems);
 int mmpfn_state_tokens(const mmpfn_ctx* ctx); /* T of the current state */
 
+/* Ensemble aggregation (classifier.py:541-566, replaces the torch post-processing):
+ * logits [M][Q][n_out]; perms [M][n_cls] int32 (NULL: no class permutation);
+ * temperature != 1 slices to n_cls and divides; average_before_softmax 0/1;
+ * class_weights [n_cls] (balance_probabilities) or NULL; probs [Q][C] with
+ * C = n_cls when sliced or permuted, else n_out. */
+int mmpfn_aggregate(mmpfn_ctx* ctx, const float* logits, int M, int Q, int n_out, const int* perms, int n_cls,
+                    float temperature, int average_before_softmax, const float* class_weights, float* probs);
+
 /* Synchronises the context stream and reports deferred device-side errors
  * (MMPFN_ERR_NAN when the embedded input held NaNs). */
 int mmpfn_status(mmpfn_ctx* ctx);

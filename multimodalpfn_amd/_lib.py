@@ -66,6 +66,7 @@ SIGNATURES = [
     ("mmpfn_copy_state", _i, [_vp, _vp, _i64]),
     ("mmpfn_state_tokens", _i, [_vp]),
     ("mmpfn_status", _i, [_vp]),
+    ("mmpfn_aggregate", _i, [_vp, _vp, _i, _i, _i, _vp, _i, _f, _i, _vp, _vp]),
     ("mmpfn_item_attention", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i]),
 ]
 

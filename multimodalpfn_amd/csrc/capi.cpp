@@ -710,6 +710,15 @@ int mmpfn_copy_state(mmpfn_ctx* ctx, float* out, int64_t cap) {
   return MMPFN_OK;
 }
 
+int mmpfn_aggregate(mmpfn_ctx* ctx, const float* logits, int M, int Q, int n_out, const int* perms, int n_cls,
+                    float temperature, int avg_before, const float* cw, float* probs) {
+  if (!ctx || !logits || !probs || M <= 0 || Q < 0 || n_out <= 0 || n_cls <= 0 || n_cls > n_out)
+    return MMPFN_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(launch_aggregate(logits, M, Q, n_out, perms, n_cls, temperature, avg_before, cw, probs, ctx->stream));
+  return MMPFN_OK;
+}
+
 int mmpfn_status(mmpfn_ctx* ctx) {
   if (!ctx) return MMPFN_ERR_INVALID;
   HIPCHK(hipSetDevice(ctx->device));

@@ -301,7 +301,72 @@ __global__ __launch_bounds__(256) void decoder_kernel(const float* __restrict__ 
   }
 }
 
+// ensemble aggregation (classifier.py:541-566): per query row, per member
+// logits[:, :n_cls] / T (if T != 1) -> class-permutation undo -> softmax -> mean
+// (or mean -> softmax), optional class re-weighting, renormalise.
+__global__ void aggregate_kernel(const float* __restrict__ logits, int M, int Q, int n_out,
+                                 const int* __restrict__ perms, int n_cls, float temp, int avg_before,
+                                 const float* __restrict__ cw, float* __restrict__ probs) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  const bool slice = temp != 1.0f;
+  const int C = (slice || perms) ? n_cls : n_out;
+  float acc[16];
+  for (int c = 0; c < C; ++c) acc[c] = 0.f;
+  for (int m = 0; m < M; ++m) {
+    const float* row = logits + ((int64_t)m * Q + q) * n_out;
+    float v[16];
+    for (int c = 0; c < C; ++c) {
+      const int src = perms ? perms[m * n_cls + c] : c;
+      v[c] = slice ? row[src] / temp : row[src];
+    }
+    if (avg_before) {
+      for (int c = 0; c < C; ++c) acc[c] += v[c];
+    } else {
+      float mx = -INFINITY;
+      for (int c = 0; c < C; ++c) mx = fmaxf(mx, v[c]);
+      float s = 0.f;
+      for (int c = 0; c < C; ++c) {
+        v[c] = expf(v[c] - mx);
+        s += v[c];
+      }
+      for (int c = 0; c < C; ++c) acc[c] += v[c] / s;
+    }
+  }
+  float out[16];
+  if (avg_before) {
+    float mx = -INFINITY;
+    for (int c = 0; c < C; ++c) mx = fmaxf(mx, acc[c] / M);
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) {
+      out[c] = expf(acc[c] / M - mx);
+      s += out[c];
+    }
+    for (int c = 0; c < C; ++c) out[c] /= s;
+  } else {
+    for (int c = 0; c < C; ++c) out[c] = acc[c] / M;
+  }
+  if (cw) {
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) {
+      out[c] *= cw[c];
+      s += out[c];
+    }
+    for (int c = 0; c < C; ++c) out[c] /= s;
+  }
+  for (int c = 0; c < C; ++c) probs[(int64_t)q * C + c] = out[c];
+}
+
 }  // namespace
+
+hipError_t launch_aggregate(const float* logits, int M, int Q, int n_out, const int* perms, int n_cls, float temp,
+                            int avg_before, const float* class_weights, float* probs, hipStream_t st) {
+  if (Q <= 0 || M <= 0) return hipSuccess;
+  if (n_out > 16 || n_cls > 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(aggregate_kernel, dim3((Q + 127) / 128), dim3(128), 0, st, logits, M, Q, n_out, perms, n_cls,
+                     temp, avg_before, class_weights, probs);
+  return hipGetLastError();
+}
 
 hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, int nf, float sigma,
                            SlotParams* slots, const float* w_enc, const float* posemb, float* X, int E, int* flag,

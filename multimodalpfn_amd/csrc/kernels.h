@@ -78,6 +78,10 @@ hipError_t launch_add_tokens(const float* tok /*[S][C][E]*/, int S, int C, const
 hipError_t launch_decoder(const float* X /*[Q][E]*/, int Q, const float* w1, const float* b1, int Fh,
                           const float* w2, const float* b2, int n_out, float* out, int E, hipStream_t st);
 
+hipError_t launch_aggregate(const float* logits /*[M][Q][n_out]*/, int M, int Q, int n_out,
+                            const int* perms /*[M][n_cls] or null*/, int n_cls, float temp, int avg_before,
+                            const float* class_weights /*[n_cls] or null*/, float* probs, hipStream_t st);
+
 // ---- mixer helpers -----------------------------------------------------------------
 hipError_t launch_layernorm_rows(const float* in, int64_t rows, int dim, float eps, void* out, bool out_f32,
                                  const float* gamma, const float* beta, hipStream_t st);

@@ -180,6 +180,25 @@ class HipEngine:
             self.status()
         return out
 
+    def aggregate(self, logits: torch.Tensor, perms, n_classes: int, temperature: float,
+                  average_before_softmax: bool, class_weights=None) -> torch.Tensor:
+        """Ensemble post-processing of classifier.py:541-566 on the device."""
+        lg = logits.to(self.device, torch.float32).contiguous()
+        M, Q, n_out = lg.shape
+        pd = None
+        if perms is not None:
+            pd = torch.as_tensor(np.asarray(perms, dtype=np.int32).reshape(M, n_classes)).to(self.device)
+        cw = None if class_weights is None else self._dev(class_weights)
+        C = n_classes if (temperature != 1 or perms is not None) else n_out
+        out = torch.empty((Q, C), device=self.device, dtype=torch.float32)
+        self._bind_stream()
+        self._check(
+            self.lib.mmpfn_aggregate(self.ctx, _ptr(lg), M, Q, n_out, _ptr(pd), n_classes, float(temperature),
+                                     int(average_before_softmax), _ptr(cw), _ptr(out)),
+            "mmpfn_aggregate",
+        )
+        return out
+
     def status(self) -> None:
         self._check(self.lib.mmpfn_status(self.ctx), "mmpfn_forward")
 

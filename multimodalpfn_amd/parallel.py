@@ -1,0 +1,59 @@
+"""Ensemble-member sharding across the GPUs of one node.
+
+Members are independent forwards (``inference.py:294-349``); the only cross-member
+step is the softmax mean (``classifier.py:555-561``).  Each rank (one process per
+GPU, ``torch.distributed`` with the ``nccl`` backend = RCCL over xGMI) runs the
+members assigned to it by greedy longest-processing-time on the cost model
+``T_m * S * N`` and contributes its fixed-size logit block to ONE all-gather.
+There is no other collective on the data path.
+"""
+
+from __future__ import annotations
+
+import heapq
+
+import torch
+
+
+def lpt_assign(costs: list[float], world: int) -> list[list[int]]:
+    """Greedy LPT: member indices per rank, heaviest first, to the least-loaded rank."""
+    heap = [(0.0, r) for r in range(world)]
+    heapq.heapify(heap)
+    out: list[list[int]] = [[] for _ in range(world)]
+    for i in sorted(range(len(costs)), key=lambda i: (-costs[i], i)):
+        load, r = heapq.heappop(heap)
+        out[r].append(i)
+        heapq.heappush(heap, (load + costs[i], r))
+    return [sorted(x) for x in out]
+
+
+def member_cost(n_tokens: int, S: int, N: int) -> float:
+    return float(n_tokens) * S * N
+
+
+def allgather_logits(local: torch.Tensor, assignment: list[list[int]], rank: int, group=None) -> torch.Tensor:
+    """Gather every rank's ``[m_r, Q, n_out]`` logits into ``[n_members, Q, n_out]`` in member order.
+
+    ``assignment`` (identical on every rank, from :func:`lpt_assign`) fixes the block
+    sizes, so this is exactly one fixed-size ``all_gather`` of ``max_r m_r`` padded
+    blocks; with one process it is a reorder.
+    """
+    import torch.distributed as dist
+
+    n_members = sum(len(a) for a in assignment)
+    tail = tuple(local.shape[1:])
+    out = torch.empty((n_members,) + tail, device=local.device, dtype=local.dtype)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        out[torch.as_tensor(assignment[rank], device=local.device, dtype=torch.long)] = local
+        return out
+    world = dist.get_world_size(group)
+    assert len(assignment) == world and local.shape[0] == len(assignment[rank])
+    m_max = max(len(a) for a in assignment)
+    pad = torch.zeros((m_max,) + tail, device=local.device, dtype=local.dtype)
+    pad[: local.shape[0]] = local
+    gathered = torch.empty((world * m_max,) + tail, device=local.device, dtype=local.dtype)
+    dist.all_gather_into_tensor(gathered, pad, group=group)
+    for r, ids in enumerate(assignment):
+        if ids:
+            out[torch.as_tensor(ids, device=local.device, dtype=torch.long)] = gathered[r * m_max : r * m_max + len(ids)]
+    return out
