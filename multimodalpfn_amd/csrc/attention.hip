@@ -223,10 +223,10 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
   float m = -INFINITY, lsum = 0.f;
 
   const int ntiles = (nk + IA_KT - 1) / IA_KT;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int it = 0; it < ntiles; ++it) {
+  const int nfull = nk / IA_KT;  // tiles with no masked key
+
+  auto tile = [&](int it, auto maskc) {
+    constexpr bool MASK = decltype(maskc)::value;
     const int k0 = it * IA_KT;
     if (it + 1 < ntiles) gload(k0 + IA_KT);
     const unsigned char* Ks = lds + (it & 1) * L::STAGE;
@@ -254,8 +254,7 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
           sacc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[ks], qf[ks], sacc[u], 0, 0, 0);
       }
     }
-    // ---- mask keys >= nk (only in the last tile)
-    if (k0 + IA_KT > nk) {
+    if constexpr (MASK) {  // keys >= nk (last tile only)
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -264,27 +263,29 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
           if (key >= nk) sacc[u][i] = -INFINITY;
         }
     }
-    // ---- online softmax (row = this lane's query; partner lane^32 holds the other keys)
-    float tm = -INFINITY;
+    // ---- online softmax (row = this lane's query; lane^32 holds the other 32 keys)
+    float tm = fmaxf(sacc[0][0], sacc[1][0]);
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) tm = fmaxf(tm, sacc[u][i]);
-    tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+    for (int i = 1; i < 16; ++i) tm = fmaxf(tm, fmaxf(sacc[0][i], sacc[1][i]));
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tm), __float_as_uint(tm), false, false);
+      tm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
     const float mn = fmaxf(m, tm);
-    const float alpha = exp2f((m - mn) * c);
     const float mc = mn * c;
+    const float alpha = BF16 ? __builtin_amdgcn_exp2f(m * c - mc) : exp2f(m * c - mc);
     m = mn;
     float ps = 0.f;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float pv = exp2f(fmaf(sacc[u][i], c, -mc));
+        const float a = fmaf(sacc[u][i], c, -mc);
+        const float pv = BF16 ? __builtin_amdgcn_exp2f(a) : exp2f(a);
         sacc[u][i] = pv;
         ps += pv;
       }
-    lsum = lsum * alpha + ps;
+    lsum = fmaf(lsum, alpha, ps);
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[i] *= alpha;
 
@@ -316,10 +317,17 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
     }
     if (it + 1 < ntiles) lstore((it + 1) & 1);
     __syncthreads();
-  }
+  };
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int it = 0; it < nfull; ++it) tile(it, std::false_type{});
+  if (nfull < ntiles) tile(nfull, std::true_type{});
 
   // ---- normalise and store O[t][s][h*32 + d]
-  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const auto lw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
+  const float ltot = __uint_as_float(lw[0]) + __uint_as_float(lw[1]);
   const float inv = 1.0f / ltot;
   if (qi < nq) {
     TE* orow = (TE*)Op + ((int64_t)t * S + qs) * (H * 32) + h * 32;

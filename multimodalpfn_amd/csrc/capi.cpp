@@ -333,6 +333,7 @@ GemmArgs gargs() {
   std::memset(&a, 0, sizeof(a));
   a.a_rdiv = 1ll << 62;
   a.a_rmul = 0;
+  a.a_rmul2 = 1;
   a.rdiv2 = 1ll << 62;
   a.ln_eps = 1e-5f;
   return a;
@@ -402,7 +403,8 @@ int run_layer(mmpfn_ctx* ctx, int l) {
   // ---- attention between features (layer.py:332-339)
   {
     GemmArgs a = gargs();
-    a.A = X, a.lda = E, a.a_rdiv = S, a.a_rmul = S;
+    // logical rows m = s*T + t (row-major over tokens) so each row's tokens are adjacent
+    a.A = X, a.lda = E, a.a_rdiv = T, a.a_rmul = 1, a.a_rmul2 = S;
     a.W = W(L.feat_qkv, L.feat_qkv_h, prec);
     a.M = (int)R, a.N = 3 * E, a.K = E;
     a.q = big, a.S = S, a.T = T, a.H = H;

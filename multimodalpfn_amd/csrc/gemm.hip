@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
     ach[i] = c & 7;
     const int64_t m = m0 + r;
     if (m < M) {
-      const int64_t mr = (m / p.a_rdiv) * p.a_rmul + p.a_roff + (m % p.a_rdiv);
+      const int64_t mr = (m / p.a_rdiv) * p.a_rmul + (m % p.a_rdiv) * p.a_rmul2 + p.a_roff;
       arow[i] = Abase + mr * p.lda * (AF32 ? 4 : 2);
     } else {
       arow[i] = nullptr;
@@ -225,67 +225,118 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
       }
     }
     return;
-  } else if constexpr (EPI == EPI_GLU) {
-    TO* C = (TO*)p.C + (int64_t)z * p.c_zstride;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t m = m0 + wm * 32 + mt * 16 + fg * 4 + r;
-          if (m >= M) continue;
-          const int na = n0 + wn * 96 + q * 32 + fr;
-          float a = acc[mt][2 * q][r] + (bias ? bias[na] : 0.f);
-          float b = acc[mt][2 * q + 1][r] + (bias ? bias[na + 16] : 0.f);
-          const int64_t oc = (n0 + wn * 96) / 2 + q * 16 + fr;
-          C[m * p.ldc + oc] = from_f32<TO>(a * sigmoidf_(b));
-        }
-    return;
   } else {
+    // Stage the finished tile (bias + activation / GLU applied) in LDS in the output
+    // dtype, then write 16-byte units ordered so that consecutive lanes hit
+    // consecutive addresses of the destination layout (4 KB runs per head for the
+    // attention scatter layouts instead of 2-byte / 32-byte fragments).
+    constexpr int OB = sizeof(TO);
+    constexpr int UE = 16 / OB;                  // elements per 16-byte unit
+    constexpr bool GLU = EPI == EPI_GLU;
+    constexpr int TCOLS = GLU ? BN / 2 : BN;     // staged columns
+    constexpr int LDC = TCOLS + UE;              // padded LDS row (elements)
+    TO* Ct = (TO*)smem;
+    __syncthreads();
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 6; ++nt)
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm * 32 + mt * 16 + fg * 4 + r;
+        if constexpr (GLU) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t m = m0 + wm * 32 + mt * 16 + fg * 4 + r;
-          if (m >= M) continue;
-          const int n = n0 + wn * 96 + nt * 16 + fr;
-          float v = acc[mt][nt][r] + (bias ? bias[n] : 0.f);
-          if (p.act == ACT_GELU) v = gelu_erf(v);
-          if constexpr (EPI == EPI_STORE) {
-            TO* C = (TO*)p.C + (int64_t)z * p.c_zstride;
-            C[m * p.ldc + n] = from_f32<TO>(v);
-          } else if constexpr (EPI == EPI_REMAP) {
-            TO* C = (TO*)p.C;
-            const int64_t dr = (m / p.rdiv2) * p.rmul2 + (int64_t)z * p.zmul + (m % p.rdiv2);
-            C[dr * p.ldc + n] = from_f32<TO>(v);
-          } else if constexpr (EPI == EPI_ITEM_QKV) {
-            const int64_t t = m / p.a_rdiv, s = p.a_roff + m % p.a_rdiv;
-            const int E = p.H * 32;
-            const int j = n / E, h = (n % E) >> 5, d = n & 31;
-            const int64_t th = t * p.H + h;
-            if (j == 0)
-              ((TO*)p.q)[(th * p.S + s) * 32 + d] = from_f32<TO>(v);
-            else if (j == 1)
-              ((TO*)p.k)[(th * p.Npad + s) * 32 + d] = from_f32<TO>(v);
-            else
-              ((TO*)p.v)[(th * 32 + d) * p.Npad + s] = from_f32<TO>(v);
-          } else if constexpr (EPI == EPI_FEAT_QKV) {
-            const int64_t t = m / p.a_rdiv, s = m % p.a_rdiv;
-            const int E = p.H * 32;
-            const int j = n / E, h = (n % E) >> 5, d = n & 31;
-            ((TO*)p.q)[(((s * 3 + j) * p.H + h) * p.T + t) * 32 + d] = from_f32<TO>(v);
+          for (int q = 0; q < 3; ++q) {
+            const int na = n0 + wn * 96 + q * 32 + fr;
+            const float a = acc[mt][2 * q][r] + (bias ? bias[na] : 0.f);
+            const float b = acc[mt][2 * q + 1][r] + (bias ? bias[na + 16] : 0.f);
+            Ct[rl * LDC + wn * 48 + q * 16 + fr] = from_f32<TO>(a * sigmoidf_(b));
+          }
+        } else {
+#pragma unroll
+          for (int nt = 0; nt < 6; ++nt) {
+            const int cl = wn * 96 + nt * 16 + fr;
+            float v = acc[mt][nt][r] + (bias ? bias[n0 + cl] : 0.f);
+            if (p.act == ACT_GELU) v = gelu_erf(v);
+            Ct[rl * LDC + cl] = from_f32<TO>(v);
           }
         }
+      }
+    __syncthreads();
+    const int E = p.H * 32;
+    const bool vt_block = (EPI == EPI_ITEM_QKV) && (n0 / 192 == 2);
+    if (!vt_block) {
+      constexpr int CPB = 32 / UE;  // units per 32-column block per row
+      constexpr int UNITS = BM * TCOLS / UE;
+      for (int u = tid; u < UNITS; u += 256) {
+        const int cb = u / (BM * CPB), rem = u % (BM * CPB);
+        const int rl = rem / CPB, cl = cb * 32 + (rem % CPB) * UE;
+        const int64_t m = m0 + rl;
+        if (m >= M) continue;
+        const u32x4 val = *(const u32x4*)(Ct + rl * LDC + cl);
+        TO* dst;
+        if constexpr (EPI == EPI_STORE) {
+          dst = (TO*)p.C + (int64_t)z * p.c_zstride + m * p.ldc + n0 + cl;
+        } else if constexpr (EPI == EPI_GLU) {
+          dst = (TO*)p.C + (int64_t)z * p.c_zstride + m * p.ldc + n0 / 2 + cl;
+        } else if constexpr (EPI == EPI_REMAP) {
+          const int64_t dr = (m / p.rdiv2) * p.rmul2 + (int64_t)z * p.zmul + (m % p.rdiv2);
+          dst = (TO*)p.C + dr * p.ldc + n0 + cl;
+        } else if constexpr (EPI == EPI_FEAT_QKV) {
+          const int n = n0 + cl;
+          const int j = n / E, h = (n % E) >> 5, d = n & 31;
+          const int64_t s = m / p.a_rdiv, t = m % p.a_rdiv;
+          dst = (TO*)p.q + (((s * 3 + j) * p.H + h) * p.T + t) * 32 + d;
+        } else {  // EPI_ITEM_QKV, Q or K block
+          const int n = n0 + cl;
+          const int j = n / E, h = (n % E) >> 5, d = n & 31;
+          const int64_t t = m / p.a_rdiv, s = p.a_roff + m % p.a_rdiv;
+          const int64_t th = t * p.H + h;
+          dst = j == 0 ? (TO*)p.q + (th * p.S + s) * 32 + d : (TO*)p.k + (th * p.Npad + s) * 32 + d;
+        }
+        *(u32x4*)dst = val;
+      }
+    } else {
+      // V^T [T][H][32][Npad]: units of UE consecutive rows s of one (h, d) column
+      constexpr int RPC = BM / UE;  // units per column
+      for (int u = tid; u < BN * RPC; u += 256) {
+        const int cl = u / RPC, rc = u % RPC;
+        const int n = n0 + cl;
+        const int h = (n % E) >> 5, d = n & 31;
+        const int64_t ma = m0 + rc * UE;
+        if (ma >= M) continue;
+        const int64_t mb = ma + UE - 1;
+        const int64_t ta = ma / p.a_rdiv, sa = p.a_roff + ma % p.a_rdiv;
+        if (mb < M && mb / p.a_rdiv == ta && (sa % UE) == 0) {
+          TO* dst = (TO*)p.v + ((ta * p.H + h) * 32 + d) * p.Npad + sa;
+          if constexpr (OB == 2) {
+            bf16x8 w;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w[i] = Ct[(rc * UE + i) * LDC + cl];
+            *(bf16x8*)dst = w;
+          } else {
+            f32x4 w;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[i] = Ct[(rc * UE + i) * LDC + cl];
+            *(f32x4*)dst = w;
+          }
+        } else {
+          for (int i = 0; i < UE; ++i) {
+            const int64_t m = ma + i;
+            if (m >= M) break;
+            const int64_t t = m / p.a_rdiv, s = p.a_roff + m % p.a_rdiv;
+            ((TO*)p.v)[((t * p.H + h) * 32 + d) * p.Npad + s] = Ct[(rc * UE + i) * LDC + cl];
+          }
+        }
+      }
+    }
   }
 }
 
 template <bool BF16, bool AF32, bool OF32, int EPI>
 hipError_t launch_t(const GemmArgs& a, int groups, hipStream_t st) {
   dim3 grid((a.M + BM - 1) / BM, a.N / BN, groups);
-  const int lds = EPI == EPI_RES_LN ? (LDS_LN > LDS_STAGE ? LDS_LN : LDS_STAGE) : LDS_STAGE;
+  constexpr int OUTB = (EPI == EPI_RES_LN || OF32) ? 4 : 2;
+  constexpr int STAGED = EPI == EPI_RES_LN ? LDS_LN : BM * (BN + 16 / OUTB) * OUTB;
+  const int lds = STAGED > LDS_STAGE ? STAGED : LDS_STAGE;
   hipLaunchKernelGGL((gemm_kernel<BF16, AF32, OF32, EPI>), grid, dim3(256), lds, st, a);
   return hipGetLastError();
 }

@@ -10,7 +10,7 @@ enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1 };
 enum Epi : int {
   EPI_STORE = 0,      // C[row] = act(acc + bias)
   EPI_ITEM_QKV = 1,   // scatter to item-attention Q / K / V^T layouts
-  EPI_FEAT_QKV = 2,   // scatter to feature-attention [S][3][H][T][d] layout
+  EPI_FEAT_QKV = 2,   // scatter to feature-attention [S][3][H][T][d] layout (rows m = s*T + t)
   EPI_RES_LN = 3,     // X[row] = LayerNorm(X[row] + acc), N == 192 (no affine)
   EPI_GLU = 4,        // paired tiles: out = a * sigmoid(b) (weights row-interleaved)
   EPI_REMAP = 5,      // grouped: dest row = (m / rdiv2) * rmul2 + z * zmul + m % rdiv2
@@ -19,10 +19,10 @@ enum Epi : int {
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1 };
 
 struct GemmArgs {
-  // A: logical row m -> memory row (m / a_rdiv) * a_rmul + a_roff + (m % a_rdiv)
+  // A: logical row m -> memory row (m / a_rdiv) * a_rmul + (m % a_rdiv) * a_rmul2 + a_roff
   const void* A;
   int64_t lda;
-  int64_t a_rdiv, a_rmul, a_roff;
+  int64_t a_rdiv, a_rmul, a_rmul2, a_roff;
   int64_t a_zstride;  // elements between groups (blockIdx.z)
   const void* W;      // [N][K] compute dtype, row-major
   int64_t w_zstride;
