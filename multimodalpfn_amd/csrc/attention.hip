@@ -119,6 +119,17 @@ struct IaLds {
   static constexpr int STAGE = KBYTES + VBYTES;
 };
 
+// Softmax bookkeeping (per lane = per query, log2 domain, Q pre-scaled by log2(e)/sqrt(d)):
+//   m_ref : reference max; S^T accumulators start from -m_ref (a persistent 16-register
+//           vector), so the MFMA chain itself yields s - m_ref and p = exp2(acc) needs no
+//           extra VALU op.
+//   lazy rescale: m_ref only moves when a tile's max exceeds it by more than TAU
+//           (p <= 2^TAU, safe in bf16/fp32) -- wave-uniform branch, rare after the
+//           first tiles; the first tile always sets m_ref.
+//   row sum (bf16 path): an extra MFMA with an all-ones A operand accumulates
+//           sum_k p into every register of lacc, moving the adds off the VALU.
+constexpr float IA_TAU = 8.0f;
+
 template <bool BF16>
 __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__ Qp, const void* __restrict__ Kp,
                                                         const void* __restrict__ Vp, void* __restrict__ Op, int S,
@@ -143,24 +154,33 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
   const int qi = blockIdx.x * IA_QB + wave * 32 + r;  // query offset in [0, nq)
   const int64_t qs = s0 + min(qi, nq - 1);
 
-  // ---- Q fragments (B operand of S^T = K Q^T)
+  // ---- Q fragments (B operand of S^T = K Q^T), pre-scaled by c
   bf16x8 qb[2];
   float qf[16];
   if constexpr (BF16) {
     const bf16* qrow = (const bf16*)Q + qs * 32;
-    qb[0] = *(const bf16x8*)(qrow + 8 * hh);
-    qb[1] = *(const bf16x8*)(qrow + 16 + 8 * hh);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 raw = *(const bf16x8*)(qrow + 16 * ks + 8 * hh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qb[ks][j] = (bf16)((float)raw[j] * c);
+    }
   } else {
     const float* qrow = (const float*)Q + qs * 32 + 16 * hh;
 #pragma unroll
     for (int i = 0; i < 16; i += 4) *(f32x4*)(qf + i) = *(const f32x4*)(qrow + i);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) qf[i] *= c;
   }
 
   // ---- staging: K tile [64][32], V^T tile [32][64]
   constexpr int KCH = IA_KT * 32 * EB / 16 / 256;  // 16-byte chunks per thread (K)
   constexpr int VCH = 32 * IA_KT * EB / 16 / 256;
+  constexpr int VCPR = IA_KT * EB / 16;            // chunks per V^T row
+  constexpr int EPC = 16 / EB;                     // elements per chunk
   u32x4 rk[KCH], rv[VCH];
-  auto gload = [&](int k0) {
+  auto gload = [&](int k0, auto maskc) {
+    constexpr bool MASKV = decltype(maskc)::value;
 #pragma unroll
     for (int i = 0; i < KCH; ++i) {
       const int cidx = tid + 256 * i;  // chunk over the contiguous K tile
@@ -169,13 +189,10 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
       const int cidx = tid + 256 * i;
-      constexpr int CPR = IA_KT * EB / 16;  // chunks per V^T row
-      const int d = cidx / CPR, ch = cidx % CPR;
+      const int d = cidx / VCPR, ch = cidx % VCPR;
       rv[i] = *(const u32x4*)((const unsigned char*)(Vg + (int64_t)d * Npad + k0) + ch * 16);
-      // zero V for keys >= nk so masked (p = 0) columns never meet stale NaN/inf
-      constexpr int EPC = 16 / EB;
-      const int kfirst = k0 + ch * EPC;
-      if (kfirst + EPC > nk) {
+      if constexpr (MASKV) {  // zero V for keys >= nk: masked p = 0 must never meet NaN/inf
+        const int kfirst = k0 + ch * EPC;
         if constexpr (BF16) {
           bf16x8 e = __builtin_bit_cast(bf16x8, rv[i]);
 #pragma unroll
@@ -205,8 +222,7 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
       const int cidx = tid + 256 * i;
-      constexpr int CPR = IA_KT * EB / 16;
-      const int d = cidx / CPR, ch = cidx % CPR;
+      const int d = cidx / VCPR, ch = cidx % VCPR;
       unsigned char* dst = Vs + d * L::VROW + ch * 16;
       if constexpr (BF16) {  // 136-byte rows are 8-byte aligned only
         *(u32x2*)dst = u32x2{rv[i].x, rv[i].y};
@@ -217,40 +233,45 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
     }
   };
 
-  f32x16 o;
+  f32x16 o, lacc, negm;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) o[i] = 0.f;
-  float m = -INFINITY, lsum = 0.f;
+  for (int i = 0; i < 16; ++i) o[i] = lacc[i] = negm[i] = 0.f;
+  float mref = 0.f, lsum = 0.f;
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
 
   const int ntiles = (nk + IA_KT - 1) / IA_KT;
-  const int nfull = nk / IA_KT;  // tiles with no masked key
+  const bool partial = (nk % IA_KT) != 0;
 
-  auto tile = [&](int it, auto maskc) {
+  auto tile = [&](int it, auto maskc, auto firstc) {
     constexpr bool MASK = decltype(maskc)::value;
+    constexpr bool FIRST = decltype(firstc)::value;
     const int k0 = it * IA_KT;
-    if (it + 1 < ntiles) gload(k0 + IA_KT);
+    if (it + 1 < ntiles) {
+      if (partial && it + 2 == ntiles) gload(k0 + IA_KT, std::true_type{});
+      else gload(k0 + IA_KT, std::false_type{});
+    }
     const unsigned char* Ks = lds + (it & 1) * L::STAGE;
     const unsigned char* Vs = Ks + L::KBYTES;
 
-    // ---- S^T for the two 32-key subtiles
+    // ---- S^T - m_ref for the two 32-key subtiles
     f32x16 sacc[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[u][i] = 0.f;
       const unsigned char* krow = Ks + (32 * u + r) * L::KROW;
       if constexpr (BF16) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const bf16x8 ka = *(const bf16x8*)(krow + (16 * ks + 8 * hh) * 2);
-          sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qb[ks], sacc[u], 0, 0, 0);
-        }
+        const bf16x8 k0f = *(const bf16x8*)(krow + (8 * hh) * 2);
+        const bf16x8 k1f = *(const bf16x8*)(krow + (16 + 8 * hh) * 2);
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0f, qb[0], negm, 0, 0, 0);
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1f, qb[1], sacc[u], 0, 0, 0);
       } else {
         float kf[16];
 #pragma unroll
         for (int i = 0; i < 16; i += 4) *(f32x4*)(kf + i) = *(const f32x4*)(krow + (16 * hh + i) * 4);
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[0], qf[0], negm, 0, 0, 0);
 #pragma unroll
-        for (int ks = 0; ks < 16; ++ks)
+        for (int ks = 1; ks < 16; ++ks)
           sacc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[ks], qf[ks], sacc[u], 0, 0, 0);
       }
     }
@@ -263,7 +284,7 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
           if (key >= nk) sacc[u][i] = -INFINITY;
         }
     }
-    // ---- online softmax (row = this lane's query; lane^32 holds the other 32 keys)
+    // ---- tile max relative to m_ref (lane^32 holds the other 32 keys of this query)
     float tm = fmaxf(sacc[0][0], sacc[1][0]);
 #pragma unroll
     for (int i = 1; i < 16; ++i) tm = fmaxf(tm, fmaxf(sacc[0][i], sacc[1][i]));
@@ -271,25 +292,28 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tm), __float_as_uint(tm), false, false);
       tm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
     }
-    const float mn = fmaxf(m, tm);
-    const float mc = mn * c;
-    const float alpha = BF16 ? __builtin_amdgcn_exp2f(m * c - mc) : exp2f(m * c - mc);
-    m = mn;
-    float ps = 0.f;
+    if (FIRST || __any(tm > IA_TAU)) {  // wave-uniform lazy rescale
+      const float delta = FIRST ? tm : fmaxf(tm, 0.f);
+      if constexpr (!FIRST) {
+        const float alpha = exp2f(-delta);
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+        for (int i = 0; i < 16; ++i) o[i] *= alpha;
+        if constexpr (BF16) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) lacc[i] *= alpha;
+        } else {
+          lsum *= alpha;
+        }
+      }
+      mref += delta;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float a = fmaf(sacc[u][i], c, -mc);
-        const float pv = BF16 ? __builtin_amdgcn_exp2f(a) : exp2f(a);
-        sacc[u][i] = pv;
-        ps += pv;
+        negm[i] = -mref;
+        sacc[0][i] -= delta;
+        sacc[1][i] -= delta;
       }
-    lsum = fmaf(lsum, alpha, ps);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) o[i] *= alpha;
-
-    // ---- O^T += V^T . P^T
+    }
+    // ---- p = exp2(s - m_ref), O^T += V^T . P^T, l += 1 . P^T
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const unsigned char* vrow = Vs + r * L::VROW;
@@ -298,14 +322,20 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
         for (int sp = 0; sp < 2; ++sp) {
           bf16x8 pb;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) pb[j] = (bf16)sacc[u][8 * sp + j];
+          for (int j = 0; j < 8; ++j) pb[j] = (bf16)__builtin_amdgcn_exp2f(sacc[u][8 * sp + j]);
           const int kb = 32 * u + 16 * sp + 4 * hh;
           const u32x2 v0 = *(const u32x2*)(vrow + kb * 2);
           const u32x2 v1 = *(const u32x2*)(vrow + (kb + 8) * 2);
           const bf16x8 va = __builtin_bit_cast(bf16x8, u32x4{v0.x, v0.y, v1.x, v1.y});
           o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o, 0, 0, 0);
+          lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pb, lacc, 0, 0, 0);
         }
       } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          sacc[u][i] = exp2f(sacc[u][i]);
+          lsum += sacc[u][i];
+        }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const f32x4 vv = *(const f32x4*)(vrow + (32 * u + 8 * g + 4 * hh) * 4);
@@ -319,15 +349,27 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
     __syncthreads();
   };
 
-  gload(0);
+  gload(0, std::bool_constant<true>{});  // masking is a no-op unless the tile is partial
   lstore(0);
   __syncthreads();
-  for (int it = 0; it < nfull; ++it) tile(it, std::false_type{});
-  if (nfull < ntiles) tile(nfull, std::true_type{});
+  if (ntiles == 1) {
+    if (partial) tile(0, std::true_type{}, std::true_type{});
+    else tile(0, std::false_type{}, std::true_type{});
+  } else {
+    tile(0, std::false_type{}, std::true_type{});
+    const int nfull = nk / IA_KT;
+    for (int it = 1; it < nfull; ++it) tile(it, std::false_type{}, std::false_type{});
+    if (partial) tile(nfull, std::true_type{}, std::false_type{});
+  }
 
   // ---- normalise and store O[t][s][h*32 + d]
-  const auto lw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
-  const float ltot = __uint_as_float(lw[0]) + __uint_as_float(lw[1]);
+  float ltot;
+  if constexpr (BF16) {
+    ltot = lacc[0];
+  } else {
+    const auto lw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
+    ltot = __uint_as_float(lw[0]) + __uint_as_float(lw[1]);
+  }
   const float inv = 1.0f / ltot;
   if (qi < nq) {
     TE* orow = (TE*)Op + ((int64_t)t * S + qs) * (H * 32) + h * 32;

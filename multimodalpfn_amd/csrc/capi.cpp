@@ -361,7 +361,7 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
   const size_t R = (size_t)S * T;
   RC(ensure(ctx, ctx->ws_X, R * E * 4));
   RC(ensure(ctx, ctx->ws_O, R * E * 4));
-  const size_t big = std::max(R * d.nhid, R * E + (size_t)2 * T * Npad * E) * 4;
+  const size_t big = std::max(R * 3 * E, R * E + (size_t)2 * T * Npad * E) * 4;
   RC(ensure(ctx, ctx->ws_big, big));
   RC(ensure(ctx, ctx->ws_pe, (size_t)(G + C + 1) * E * 4));
   RC(ensure(ctx, ctx->ws_slots, (size_t)(G + 1) * fpg * sizeof(SlotParams)));
@@ -440,18 +440,8 @@ int run_layer(mmpfn_ctx* ctx, int l) {
     b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
     HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
   }
-  // ---- MLP (mlp.py:93-104)
-  {
-    GemmArgs a = gargs();
-    a.A = X, a.lda = E, a.W = W(L.mlp1, L.mlp1_h, prec);
-    a.M = (int)R, a.N = d.nhid, a.K = E, a.act = ACT_GELU;
-    a.C = big, a.ldc = d.nhid;
-    HIPCHK(launch_gemm(a, prec, EPI_STORE, true, !bf, 1, st));
-    GemmArgs b = gargs();
-    b.A = big, b.lda = d.nhid, b.W = W(L.mlp2, L.mlp2_h, prec);
-    b.M = (int)R, b.N = E, b.K = d.nhid, b.X = X, b.ln_eps = d.ln_eps;
-    HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
-  }
+  // ---- MLP (mlp.py:93-104), fused up/GELU/down/residual/LN
+  HIPCHK(launch_mlp_fused(X, W(L.mlp1, L.mlp1_h, prec), W(L.mlp2, L.mlp2_h, prec), R, E, d.nhid, d.ln_eps, prec, st));
   return MMPFN_OK;
 }
 

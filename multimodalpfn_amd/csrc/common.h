@@ -34,9 +34,33 @@ template <typename T> __device__ __forceinline__ T from_f32(float x);
 template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
 
-// exact GELU (torch default, approximate='none')
+// erf, branch-free (Abramowitz & Stegun 7.1.26, |abs err| <= 1.5e-7): the libm
+// erff is a multi-branch routine that dominated the MLP epilogue.
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = __builtin_amdgcn_exp2f(-ax * ax * 1.4426950408889634f);
+  return copysignf(fmaf(-p, e, 1.0f), x);
+}
+
+// GELU with the exact-erf formulation (torch default, approximate='none')
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+  return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
+}
+
+// tanh-form GELU, x * sigmoid(2 sqrt(2/pi) (x + 0.044715 x^3)): |err| <= 3e-4, below the
+// bf16 resolution of the activations it feeds; 7 VALU ops (2 transcendental).  Used
+// only on the bf16 performance path; the fp32 parity path keeps gelu_erf.
+__device__ __forceinline__ float gelu_tanh_fast(float x) {
+  const float k = -2.0f * 0.7978845608028654f * 1.4426950408889634f;  // -2 sqrt(2/pi) log2(e)
+  const float x2 = x * x;
+  const float u = x * fmaf(k * 0.044715f, x2, k);
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }

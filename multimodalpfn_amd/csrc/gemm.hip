@@ -190,7 +190,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
           const int cl = wn * 96 + nt * 16 + fr;
           const int64_t m = m0 + rl;
           float v = acc[mt][nt][r] + (bias ? bias[cl] : 0.f);
-          if (m < M) v += p.X[m * 192 + cl];
+          const float xr = p.X[min(m, (int64_t)M - 1) * 192 + cl];
+          v += (m < M) ? xr : 0.f;
           Es[rl * LN_STRIDE + cl] = v;
         }
     __syncthreads();

@@ -50,6 +50,10 @@ struct GemmArgs {
 hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool out_f32, int groups,
                        hipStream_t st);
 
+// fused MLP sublayer: X <- LN(X + GELU(X W1^T) W2^T), W1 [Fh][E], W2 [E][Fh] in compute dtype
+hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M, int E, int Fh, float eps, int prec,
+                            hipStream_t st);
+
 // ---- attention -------------------------------------------------------------------
 // feature attention: qkv [S][3][H][T][d], out O [T][S][H*d]
 hipError_t launch_attn_feature(const void* qkv, void* out, int S, int T, int H, int prec, hipStream_t st);
