@@ -1,12 +1,13 @@
 // Attention kernels of the PerFeatureEncoderLayer (layer.py:332-395,
 // multi_head_attention.py:547-736) for gfx950.
 //
-// 1. attn_feature: self-attention over the T tokens of every row s (feature axis).
-//    T is small (tens to a few hundred); one 256-thread block per row, one thread per
-//    (head, query token), K/V staged through LDS in 32-key chunks, chunked online
-//    softmax in fp32 on the VALU.
+// One MFMA flash-attention kernel serves both axes:
+//  * sample axis (attn_between_items): batch = token column t, queries = rows s,
+//    4 waves x 32 queries per block -- the dominant cost of the forward;
+//  * feature axis (attn_between_features): batch = row s, queries = keys = the T
+//    tokens of that row, one wave per block.
 //
-// 2. attn_item: the sample-axis flash attention -- the dominant cost of the forward.
+// Sample-axis details:
 //    For token column t and head h, query rows s in [s0, s0+nq) attend to keys
 //    [0, nk) (the train rows).  Train queries use their own head's K/V; test queries
 //    use head 0's K/V for every head (reuse_first_head_kv, layer.py:344-358) via
@@ -26,89 +27,8 @@ namespace mmpfn {
 
 namespace {
 
-// ------------------------------------------------------------------ feature attention
-constexpr int FA_KC = 32;  // keys per LDS chunk
-
-template <typename TI, typename TO>
-__global__ __launch_bounds__(256) void attn_feature_kernel(const TI* __restrict__ qkv, TO* __restrict__ out,
-                                                           int S, int T, int H) {
-  __shared__ float Ks[6 * FA_KC * 33];  // [H][KC][32+1]
-  __shared__ float Vs[6 * FA_KC * 33];
-  const int s = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int64_t slab = (int64_t)H * T * 32;  // elements per (s, j)
-  const TI* qb = qkv + (int64_t)s * 3 * slab;
-  const TI* kb = qb + slab;
-  const TI* vb = qb + 2 * slab;
-  const float scale = 0.17677669529663687f;  // 1/sqrt(32)
-  const int npairs = H * T;
-  for (int pb = 0; pb < npairs; pb += 256) {
-    const int pair = pb + tid;
-    const bool active = pair < npairs;
-    const int h = active ? pair / T : 0, tq = active ? pair % T : 0;
-    float q[32], acc[32];
-    const TI* qr = qb + ((int64_t)h * T + tq) * 32;
-#pragma unroll
-    for (int d = 0; d < 32; ++d) {
-      q[d] = to_f32(qr[d]) * scale;
-      acc[d] = 0.f;
-    }
-    float m = -INFINITY, l = 0.f;
-    for (int k0 = 0; k0 < T; k0 += FA_KC) {
-      const int kc = min(FA_KC, T - k0);
-      __syncthreads();
-      for (int i = tid; i < H * kc * 32; i += 256) {
-        const int hh = i / (kc * 32), rem = i % (kc * 32), kk = rem >> 5, d = rem & 31;
-        const int64_t gi = ((int64_t)hh * T + k0 + kk) * 32 + d;
-        Ks[(hh * FA_KC + kk) * 33 + d] = to_f32(kb[gi]);
-        Vs[(hh * FA_KC + kk) * 33 + d] = to_f32(vb[gi]);
-      }
-      __syncthreads();
-      if (active) {
-        float sc[FA_KC];
-        float cm = -INFINITY;
-#pragma unroll
-        for (int kk = 0; kk < FA_KC; ++kk) {
-          float a = -INFINITY;
-          if (kk < kc) {
-            const float* kr = Ks + (h * FA_KC + kk) * 33;
-            a = 0.f;
-#pragma unroll
-            for (int d = 0; d < 32; ++d) a = fmaf(q[d], kr[d], a);
-          }
-          sc[kk] = a;
-          cm = fmaxf(cm, a);
-        }
-        const float mn = fmaxf(m, cm);
-        const float corr = expf(m - mn);
-        l *= corr;
-#pragma unroll
-        for (int d = 0; d < 32; ++d) acc[d] *= corr;
-#pragma unroll
-        for (int kk = 0; kk < FA_KC; ++kk) {
-          if (kk < kc) {
-            const float pexp = expf(sc[kk] - mn);
-            l += pexp;
-            const float* vr = Vs + (h * FA_KC + kk) * 33;
-#pragma unroll
-            for (int d = 0; d < 32; ++d) acc[d] = fmaf(pexp, vr[d], acc[d]);
-          }
-        }
-        m = mn;
-      }
-    }
-    if (active) {
-      const float inv = 1.0f / l;
-      TO* orow = out + ((int64_t)tq * S + s) * (H * 32) + h * 32;
-#pragma unroll
-      for (int d = 0; d < 32; ++d) orow[d] = from_f32<TO>(acc[d] * inv);
-    }
-  }
-}
-
 // ------------------------------------------------------------------ item attention
 constexpr int IA_KT = 64;          // keys per LDS tile
-constexpr int IA_QB = 128;         // queries per block (4 waves x 32)
 
 template <bool BF16>
 struct IaLds {
@@ -130,11 +50,8 @@ struct IaLds {
 //           sum_k p into every register of lacc, moving the adds off the VALU.
 constexpr float IA_TAU = 8.0f;
 
-template <bool BF16>
-__global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__ Qp, const void* __restrict__ Kp,
-                                                        const void* __restrict__ Vp, void* __restrict__ Op, int S,
-                                                        int T, int H, int Npad, int s0, int nq, int nk,
-                                                        int kvh_fixed) {
+template <bool BF16, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
   typedef typename std::conditional<BF16, bf16, float>::type TE;
   constexpr int EB = sizeof(TE);
   using L = IaLds<BF16>;
@@ -142,16 +59,16 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int h = blockIdx.y, t = blockIdx.z;
-  const int kvh = kvh_fixed >= 0 ? kvh_fixed : h;
-  const int64_t thq = (int64_t)t * H + h;
-  const int64_t thk = (int64_t)t * H + kvh;
-  const TE* Q = (const TE*)Qp + thq * S * 32;
-  const TE* Kg = (const TE*)Kp + thk * (int64_t)Npad * 32;
-  const TE* Vg = (const TE*)Vp + thk * 32 * (int64_t)Npad;
+  constexpr int NT = 64 * NW;  // threads per block
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int kvh = p.kvh_fixed >= 0 ? p.kvh_fixed : h;
+  const int s0 = p.s0, nq = p.nq, nk = p.nk, Npad = p.kpad;
+  const TE* Q = (const TE*)p.q + b * p.q_bstride + h * p.q_hstride;
+  const TE* Kg = (const TE*)p.k + b * p.kv_bstride + kvh * p.kv_hstride;
+  const TE* Vg = (const TE*)p.vt + b * p.kv_bstride + kvh * p.kv_hstride;
   const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
 
-  const int qi = blockIdx.x * IA_QB + wave * 32 + r;  // query offset in [0, nq)
+  const int qi = blockIdx.x * (32 * NW) + wave * 32 + r;  // query offset in [0, nq)
   const int64_t qs = s0 + min(qi, nq - 1);
 
   // ---- Q fragments (B operand of S^T = K Q^T), pre-scaled by c
@@ -174,8 +91,8 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
   }
 
   // ---- staging: K tile [64][32], V^T tile [32][64]
-  constexpr int KCH = IA_KT * 32 * EB / 16 / 256;  // 16-byte chunks per thread (K)
-  constexpr int VCH = 32 * IA_KT * EB / 16 / 256;
+  constexpr int KCH = IA_KT * 32 * EB / 16 / NT;  // 16-byte chunks per thread (K)
+  constexpr int VCH = 32 * IA_KT * EB / 16 / NT;
   constexpr int VCPR = IA_KT * EB / 16;            // chunks per V^T row
   constexpr int EPC = 16 / EB;                     // elements per chunk
   u32x4 rk[KCH], rv[VCH];
@@ -183,12 +100,12 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
     constexpr bool MASKV = decltype(maskc)::value;
 #pragma unroll
     for (int i = 0; i < KCH; ++i) {
-      const int cidx = tid + 256 * i;  // chunk over the contiguous K tile
+      const int cidx = tid + NT * i;  // chunk over the contiguous K tile
       rk[i] = *(const u32x4*)((const unsigned char*)(Kg + (int64_t)k0 * 32) + cidx * 16);
     }
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
-      const int cidx = tid + 256 * i;
+      const int cidx = tid + NT * i;
       const int d = cidx / VCPR, ch = cidx % VCPR;
       rv[i] = *(const u32x4*)((const unsigned char*)(Vg + (int64_t)d * Npad + k0) + ch * 16);
       if constexpr (MASKV) {  // zero V for keys >= nk: masked p = 0 must never meet NaN/inf
@@ -214,14 +131,14 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
     unsigned char* Vs = Ks + L::KBYTES;
 #pragma unroll
     for (int i = 0; i < KCH; ++i) {
-      const int cidx = tid + 256 * i;
+      const int cidx = tid + NT * i;
       constexpr int CPR = 32 * EB / 16;  // chunks per K row
       const int row = cidx / CPR, ch = cidx % CPR;
       *(u32x4*)(Ks + row * L::KROW + ch * 16) = rk[i];
     }
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
-      const int cidx = tid + 256 * i;
+      const int cidx = tid + NT * i;
       const int d = cidx / VCPR, ch = cidx % VCPR;
       unsigned char* dst = Vs + d * L::VROW + ch * 16;
       if constexpr (BF16) {  // 136-byte rows are 8-byte aligned only
@@ -372,7 +289,7 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
   }
   const float inv = 1.0f / ltot;
   if (qi < nq) {
-    TE* orow = (TE*)Op + ((int64_t)t * S + qs) * (H * 32) + h * 32;
+    TE* orow = (TE*)p.o + (b * p.o_bstride + qs * p.o_qstride) * (p.H * 32) + h * 32;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int d = 8 * g + 4 * hh;
@@ -393,30 +310,30 @@ __global__ __launch_bounds__(256) void attn_item_kernel(const void* __restrict__
 
 }  // namespace
 
-hipError_t launch_attn_feature(const void* qkv, void* out, int S, int T, int H, int prec, hipStream_t st) {
-  if (S <= 0) return hipSuccess;
-  if (H > 6) return hipErrorInvalidValue;
-  if (prec == PREC_BF16)
-    hipLaunchKernelGGL((attn_feature_kernel<bf16, bf16>), dim3(S), dim3(256), 0, st, (const bf16*)qkv, (bf16*)out,
-                       S, T, H);
-  else
-    hipLaunchKernelGGL((attn_feature_kernel<float, float>), dim3(S), dim3(256), 0, st, (const float*)qkv,
-                       (float*)out, S, T, H);
+hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int nw, hipStream_t st) {
+  if (a.nq <= 0 || batches <= 0) return hipSuccess;
+  if (a.nk <= 0 || a.kpad % IA_KT != 0 || a.nk > a.kpad) return hipErrorInvalidValue;
+  if (nw != 1 && nw != 4) return hipErrorInvalidValue;
+  dim3 grid((a.nq + 32 * nw - 1) / (32 * nw), a.H, batches);
+  if (prec == PREC_BF16) {
+    if (nw == 4) hipLaunchKernelGGL((attn_item_kernel<true, 4>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_item_kernel<true, 1>), grid, dim3(64), 0, st, a);
+  } else {
+    if (nw == 4) hipLaunchKernelGGL((attn_item_kernel<false, 4>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_item_kernel<false, 1>), grid, dim3(64), 0, st, a);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                             int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st) {
-  if (nq <= 0) return hipSuccess;
-  if (nk <= 0 || Npad % IA_KT != 0 || nk > Npad) return hipErrorInvalidValue;
-  dim3 grid((nq + IA_QB - 1) / IA_QB, H, T);
-  if (prec == PREC_BF16)
-    hipLaunchKernelGGL((attn_item_kernel<true>), grid, dim3(256), 0, st, q, k, vt, out, S, T, H, Npad, s0, nq, nk,
-                       kv_head_fixed);
-  else
-    hipLaunchKernelGGL((attn_item_kernel<false>), grid, dim3(256), 0, st, q, k, vt, out, S, T, H, Npad, s0, nq, nk,
-                       kv_head_fixed);
-  return hipGetLastError();
+  AttnArgs a;
+  a.q = q, a.k = k, a.vt = vt, a.o = out;
+  a.q_bstride = (int64_t)H * S * 32, a.q_hstride = (int64_t)S * 32;
+  a.kv_bstride = (int64_t)H * Npad * 32, a.kv_hstride = (int64_t)Npad * 32, a.kpad = Npad;
+  a.o_bstride = S, a.o_qstride = 1;
+  a.s0 = s0, a.nq = nq, a.nk = nk, a.kvh_fixed = kv_head_fixed, a.H = H;
+  return launch_attn(a, T, prec, 4, st);
 }
 
 }  // namespace mmpfn

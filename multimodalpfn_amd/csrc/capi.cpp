@@ -153,7 +153,7 @@ void fold_ln(std::vector<float>& W, std::vector<float>& c, const float* g, const
 
 int finalize(mmpfn_ctx* ctx) {
   const mmpfn_model_desc& d = ctx->d;
-  const int E = d.emsize, H = d.nhead, HD = E, Fh = d.nhid, nf = d.encoder_features;
+  const int E = d.emsize, HD = E, Fh = d.nhid, nf = d.encoder_features;
   ctx->layers.assign(d.nlayers, LayerW{});
   for (int l = 0; l < d.nlayers; ++l) {
     const std::string p = "transformer_encoder.layers." + std::to_string(l) + ".";
@@ -361,7 +361,8 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
   const size_t R = (size_t)S * T;
   RC(ensure(ctx, ctx->ws_X, R * E * 4));
   RC(ensure(ctx, ctx->ws_O, R * E * 4));
-  const size_t big = std::max(R * 3 * E, R * E + (size_t)2 * T * Npad * E) * 4;
+  const size_t Tpad = (T + 63) / 64 * 64;
+  const size_t big = std::max(R * E + (size_t)2 * S * Tpad * E, R * E + (size_t)2 * T * Npad * E) * 4;
   RC(ensure(ctx, ctx->ws_big, big));
   RC(ensure(ctx, ctx->ws_pe, (size_t)(G + C + 1) * E * 4));
   RC(ensure(ctx, ctx->ws_slots, (size_t)(G + 1) * fpg * sizeof(SlotParams)));
@@ -400,16 +401,26 @@ int run_layer(mmpfn_ctx* ctx, int l) {
   void* O = ctx->ws_O.p;
   unsigned char* big = (unsigned char*)ctx->ws_big.p;
 
-  // ---- attention between features (layer.py:332-339)
+  // ---- attention between features (layer.py:332-339): batch = row s, T tokens
   {
+    const int Tpad = (T + 63) / 64 * 64;
+    void* Qf = big;
+    void* Kf = big + (size_t)R * E * eb;
+    void* Vf = (unsigned char*)Kf + (size_t)S * H * Tpad * 32 * eb;
     GemmArgs a = gargs();
-    // logical rows m = s*T + t (row-major over tokens) so each row's tokens are adjacent
+    // logical rows m = s*T + t: A row t*S + s; scatter batch b = s, position t
     a.A = X, a.lda = E, a.a_rdiv = T, a.a_rmul = 1, a.a_rmul2 = S;
     a.W = W(L.feat_qkv, L.feat_qkv_h, prec);
     a.M = (int)R, a.N = 3 * E, a.K = E;
-    a.q = big, a.S = S, a.T = T, a.H = H;
-    HIPCHK(launch_gemm(a, prec, EPI_FEAT_QKV, true, !bf, 1, st));
-    HIPCHK(launch_attn_feature(big, O, S, T, H, prec, st));
+    a.q = Qf, a.k = Kf, a.v = Vf, a.S = T, a.Npad = Tpad, a.T = T, a.H = H;
+    HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+    AttnArgs f;
+    f.q = Qf, f.k = Kf, f.vt = Vf, f.o = O;
+    f.q_bstride = (int64_t)H * T * 32, f.q_hstride = (int64_t)T * 32;
+    f.kv_bstride = (int64_t)H * Tpad * 32, f.kv_hstride = (int64_t)Tpad * 32, f.kpad = Tpad;
+    f.o_bstride = 1, f.o_qstride = S;  // O[t][s]
+    f.s0 = 0, f.nq = T, f.nk = T, f.kvh_fixed = -1, f.H = H;
+    HIPCHK(launch_attn(f, S, prec, 1, st));
     GemmArgs b = gargs();
     b.A = O, b.lda = E, b.W = W(L.feat_out, L.feat_out_h, prec);
     b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
@@ -570,10 +581,11 @@ mmpfn_ctx* mmpfn_create(int device, void* stream) {
 
 void mmpfn_destroy(mmpfn_ctx* ctx) {
   if (!ctx) return;
-  hipSetDevice(ctx->device);
-  hipStreamSynchronize(ctx->stream);
+  // teardown: errors here have no caller to report to
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
   auto fr = [](DevBuf& b) {
-    if (b.p) hipFree(b.p);
+    if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
   };
   for (auto& L : ctx->layers) {

@@ -281,11 +281,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
         } else if constexpr (EPI == EPI_REMAP) {
           const int64_t dr = (m / p.rdiv2) * p.rmul2 + (int64_t)z * p.zmul + (m % p.rdiv2);
           dst = (TO*)p.C + dr * p.ldc + n0 + cl;
-        } else if constexpr (EPI == EPI_FEAT_QKV) {
-          const int n = n0 + cl;
-          const int j = n / E, h = (n % E) >> 5, d = n & 31;
-          const int64_t s = m / p.a_rdiv, t = m % p.a_rdiv;
-          dst = (TO*)p.q + (((s * 3 + j) * p.H + h) * p.T + t) * 32 + d;
         } else {  // EPI_ITEM_QKV, Q or K block
           const int n = n0 + cl;
           const int j = n / E, h = (n % E) >> 5, d = n & 31;
@@ -347,7 +342,6 @@ hipError_t launch_e(const GemmArgs& a, int epi, int groups, hipStream_t st) {
   switch (epi) {
     case EPI_STORE: return launch_t<BF16, AF32, OF32, EPI_STORE>(a, groups, st);
     case EPI_ITEM_QKV: return launch_t<BF16, AF32, OF32, EPI_ITEM_QKV>(a, groups, st);
-    case EPI_FEAT_QKV: return launch_t<BF16, AF32, OF32, EPI_FEAT_QKV>(a, groups, st);
     case EPI_RES_LN: return launch_t<BF16, AF32, true, EPI_RES_LN>(a, groups, st);
     case EPI_GLU: return launch_t<BF16, AF32, OF32, EPI_GLU>(a, groups, st);
     case EPI_REMAP: return launch_t<BF16, AF32, OF32, EPI_REMAP>(a, groups, st);

@@ -9,8 +9,8 @@ enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1 };
 
 enum Epi : int {
   EPI_STORE = 0,      // C[row] = act(acc + bias)
-  EPI_ITEM_QKV = 1,   // scatter to item-attention Q / K / V^T layouts
-  EPI_FEAT_QKV = 2,   // scatter to feature-attention [S][3][H][T][d] layout (rows m = s*T + t)
+  EPI_ITEM_QKV = 1,   // scatter to attention Q / K / V^T layouts: row m -> (b = m / a_rdiv, pos = a_roff + m % a_rdiv)
+                      //   Q [b][h][pos][32] (S rows), K [b][h][pos][32] (Npad rows), V^T [b][h][32][Npad]
   EPI_RES_LN = 3,     // X[row] = LayerNorm(X[row] + acc), N == 192 (no affine)
   EPI_GLU = 4,        // paired tiles: out = a * sigmoid(b) (weights row-interleaved)
   EPI_REMAP = 5,      // grouped: dest row = (m / rdiv2) * rmul2 + z * zmul + m % rdiv2
@@ -36,9 +36,9 @@ struct GemmArgs {
   int64_t c_zstride;
   int64_t rdiv2, rmul2, zmul;
   // attention scatter
-  void* q;  // Q  [T][H][S][d]          (item) | QKV [S][3][H][T][d] (feat)
-  void* k;  // K  [T][H][Npad][d]
-  void* v;  // V^T[T][H][d][Npad]
+  void* q;  // Q  [B][H][S][d]
+  void* k;  // K  [B][H][Npad][d]
+  void* v;  // V^T[B][H][d][Npad]
   int S, Npad, T, H;
   // LN epilogue
   float* X;  // residual in / normalised out, ld = 192
@@ -55,8 +55,20 @@ hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M,
                             hipStream_t st);
 
 // ---- attention -------------------------------------------------------------------
-// feature attention: qkv [S][3][H][T][d], out O [T][S][H*d]
-hipError_t launch_attn_feature(const void* qkv, void* out, int S, int T, int H, int prec, hipStream_t st);
+// generic MFMA attention over a batch (blockIdx.z) of independent sequences:
+//   Q  [b][h][pos][32] (row = s0 + q), K [b][kvh][key][32], V^T [b][kvh][32][kpad],
+//   O row = b * o_bstride + (s0 + q) * o_qstride, element row*(H*32) + h*32 + d.
+struct AttnArgs {
+  const void* q;
+  const void* k;
+  const void* vt;
+  void* o;
+  int64_t q_bstride, q_hstride, kv_bstride, kv_hstride;
+  int kpad;
+  int64_t o_bstride, o_qstride;
+  int s0, nq, nk, kvh_fixed, H;
+};
+hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int waves_per_block, hipStream_t st);
 // item attention: queries s in [s0, s0+nq), keys [0, nk); kv_head_fixed >= 0 forces that KV head
 hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
                             int Npad, int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st);

@@ -36,51 +36,77 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ 
   }
 }
 
-// CAP core: per row s, per head: softmax(q k^T / sqrt(hd)) v with q [cap][E] shared
-// by all rows and k/v = kv[s][j][0:E] / kv[s][j][E:2E] (j < M).  One block per row.
-template <typename TK>
+// CAP core: per row s, per head h: softmax(q_h k_h^T / sqrt(hd)) v_h with the learned
+// queries q [cap][E] (in-projected, shared by all rows) and k/v = kv[s][j][0:E] /
+// kv[s][j][E:2E] for the M mixer tokens.  One block per row; keys staged through LDS
+// in 32-key chunks (coalesced); one thread per (head, query) with a chunked online
+// softmax in fp32.  HD (head dim = E / cap) is a template parameter so the per-thread
+// q / acc arrays stay in registers.
+constexpr int CAP_KC = 32;
+
+template <typename TK, int HD>
 __global__ __launch_bounds__(256) void cap_attn_kernel(const float* __restrict__ qp, const TK* __restrict__ kv,
-                                                       float* __restrict__ out, int M, int cap, int E) {
-  extern __shared__ float sc[];  // [cap][M] scores of the current head
+                                                       float* __restrict__ out, int M, int cap, int E, int kcmax) {
+  extern __shared__ float ks[];  // [kcmax][2E], kcmax <= CAP_KC
   const int s = blockIdx.x;
-  const int hd = E / cap;
-  const float scale = 1.0f / sqrtf((float)hd);
+  const int tid = threadIdx.x;
+  const float scale = 1.0f / sqrtf((float)HD);
   const TK* kvs = kv + (int64_t)s * M * 2 * E;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int h = 0; h < cap; ++h) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < cap * M; i += blockDim.x) {
-      const int c = i / M, j = i % M;
-      const float* q = qp + c * E + h * hd;
-      const TK* k = kvs + (int64_t)j * 2 * E + h * hd;
-      float a = 0.f;
-      for (int d = 0; d < hd; ++d) a = fmaf(q[d], to_f32(k[d]), a);
-      sc[i] = a * scale;
+  const int pairs = cap * cap;
+  for (int pb = 0; pb < pairs; pb += 256) {
+    const int pair = pb + tid;
+    const bool active = pair < pairs;
+    const int h = active ? pair / cap : 0, c = active ? pair % cap : 0;
+    float q[HD], acc[HD];
+#pragma unroll
+    for (int i = 0; i < HD; ++i) {
+      q[i] = qp[c * E + h * HD + i] * scale;
+      acc[i] = 0.f;
     }
-    __syncthreads();
-    for (int c = wave; c < cap; c += 4) {
-      float* row = sc + c * M;
-      float mx = -INFINITY;
-      for (int j = lane; j < M; j += 64) mx = fmaxf(mx, row[j]);
-      mx = wave_max(mx);
-      float sum = 0.f;
-      for (int j = lane; j < M; j += 64) {
-        const float e = expf(row[j] - mx);
-        row[j] = e;
-        sum += e;
+    float m = -INFINITY, l = 0.f;
+    for (int k0 = 0; k0 < M; k0 += kcmax) {
+      const int kc = min(kcmax, M - k0);
+      __syncthreads();
+      for (int i = tid; i < kc * 2 * E; i += 256) ks[i] = to_f32(kvs[(int64_t)k0 * 2 * E + i]);
+      __syncthreads();
+      if (active) {
+        float sc[CAP_KC];
+        float cm = -INFINITY;
+#pragma unroll
+        for (int kk = 0; kk < CAP_KC; ++kk) {
+          float a = -INFINITY;
+          if (kk < kc) {
+            const float* kr = ks + kk * 2 * E + h * HD;
+            a = 0.f;
+#pragma unroll
+            for (int i = 0; i < HD; ++i) a = fmaf(q[i], kr[i], a);
+          }
+          sc[kk] = a;
+          cm = fmaxf(cm, a);
+        }
+        const float mn = fmaxf(m, cm);
+        const float corr = expf(m - mn);
+        l *= corr;
+#pragma unroll
+        for (int i = 0; i < HD; ++i) acc[i] *= corr;
+#pragma unroll
+        for (int kk = 0; kk < CAP_KC; ++kk) {
+          if (kk < kc) {
+            const float pe = expf(sc[kk] - mn);
+            l += pe;
+            const float* vr = ks + kk * 2 * E + E + h * HD;
+#pragma unroll
+            for (int i = 0; i < HD; ++i) acc[i] = fmaf(pe, vr[i], acc[i]);
+          }
+        }
+        m = mn;
       }
-      sum = wave_sum(sum);
-      const float inv = 1.0f / sum;
-      for (int j = lane; j < M; j += 64) row[j] *= inv;
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < cap * hd; i += blockDim.x) {
-      const int c = i / hd, d = i % hd;
-      const float* p = sc + c * M;
-      const TK* v = kvs + E + h * hd + d;
-      float a = 0.f;
-      for (int j = 0; j < M; ++j) a = fmaf(p[j], to_f32(v[(int64_t)j * 2 * E]), a);
-      out[((int64_t)s * cap + c) * E + h * hd + d] = a;
+    if (active) {
+      const float inv = 1.0f / l;
+      float* o = out + ((int64_t)s * cap + c) * E + h * HD;
+#pragma unroll
+      for (int i = 0; i < HD; ++i) o[i] = acc[i] * inv;
     }
   }
 }
@@ -151,16 +177,35 @@ hipError_t launch_layernorm_rows(const float* in, int64_t rows, int dim, float e
   return hipGetLastError();
 }
 
+template <typename TK>
+hipError_t launch_cap_t(const float* qp, const TK* kv, float* out, int S, int M, int cap, int E, hipStream_t st) {
+  // key chunk sized to keep the staged K|V within 64 KiB of LDS
+  const int kcmax = max(1, min(CAP_KC, 65536 / (8 * E)));
+  const size_t lds = (size_t)kcmax * 2 * E * sizeof(float);
+  dim3 g(S), b(256);
+  switch (E / cap) {
+    case 96: hipLaunchKernelGGL((cap_attn_kernel<TK, 96>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 48: hipLaunchKernelGGL((cap_attn_kernel<TK, 48>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 24: hipLaunchKernelGGL((cap_attn_kernel<TK, 24>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 16: hipLaunchKernelGGL((cap_attn_kernel<TK, 16>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 12: hipLaunchKernelGGL((cap_attn_kernel<TK, 12>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 8: hipLaunchKernelGGL((cap_attn_kernel<TK, 8>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 6: hipLaunchKernelGGL((cap_attn_kernel<TK, 6>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 4: hipLaunchKernelGGL((cap_attn_kernel<TK, 4>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 3: hipLaunchKernelGGL((cap_attn_kernel<TK, 3>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 2: hipLaunchKernelGGL((cap_attn_kernel<TK, 2>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 1: hipLaunchKernelGGL((cap_attn_kernel<TK, 1>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    default: return hipErrorInvalidValue;  // cap_heads with E / cap outside the instantiated set
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_cap_attention(const float* qp, const void* kv, bool kv_f32, float* out, int S, int M, int cap, int E,
                                 hipStream_t st) {
   if (S <= 0) return hipSuccess;
-  const size_t lds = (size_t)cap * M * sizeof(float);
-  if (lds > 64 * 1024) return hipErrorInvalidValue;
-  if (kv_f32)
-    hipLaunchKernelGGL(cap_attn_kernel<float>, dim3(S), dim3(256), lds, st, qp, (const float*)kv, out, M, cap, E);
-  else
-    hipLaunchKernelGGL(cap_attn_kernel<bf16>, dim3(S), dim3(256), lds, st, qp, (const bf16*)kv, out, M, cap, E);
-  return hipGetLastError();
+  if (E % cap != 0) return hipErrorInvalidValue;
+  if (kv_f32) return launch_cap_t(qp, (const float*)kv, out, S, M, cap, E, st);
+  return launch_cap_t(qp, (const bf16*)kv, out, S, M, cap, E, st);
 }
 
 hipError_t launch_ln_add(const float* o, const float* f, const float* g, const float* b, float* out, int64_t rows,

@@ -4,8 +4,11 @@ set -o pipefail
 R=$PWD
 mkdir -p gpurun_out
 timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 > gpurun_out/pytest_gpu.log 2>&1
-echo "pytest_rc=$?" >> gpurun_out/pytest_gpu.log
+rc=$?
+echo "pytest_rc=$rc" >> gpurun_out/pytest_gpu.log
 tail -3 gpurun_out/pytest_gpu.log
+# a crash / abort / time limit means the GPU may be unhealthy: stop here
+case $rc in 0|1) ;; *) exit $rc ;; esac
 timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 1
 cat gpurun_out/bench.json
 export TMPDIR=/tmp
