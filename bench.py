@@ -52,6 +52,7 @@ def parse():
     p.add_argument("--members", type=int, default=MEMBERS_PER_GPU, help="members per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--attn-reps", type=int, default=20)
+    p.add_argument("--api-steps", type=int, default=3, help="timed predict_proba calls of the API leg (0: skip)")
     return p.parse_args()
 
 
@@ -158,6 +159,55 @@ def cpu_baseline(sd, x, y, image):
     }
 
 
+def api_end_to_end(cfg, sd, x, y, image, n_estimators, prec_f32, steps, world):
+    """``MMPFNClassifier.predict_proba`` wall time from host numpy inputs (PCIe-inclusive).
+
+    run.py's interface config (no preprocessing, no fingerprint), the 18 categorical
+    columns marked, ``n_estimators`` members (sharded over ranks when distributed).
+    """
+    import tempfile
+
+    import torch.distributed as dist
+
+    from multimodalpfn_amd import MMPFNClassifier
+    from multimodalpfn_amd.constants import ModelInterfaceConfig
+    from multimodalpfn_amd.preprocessing import PreprocessorConfig
+    from api_cases import ckpt_config
+
+    with tempfile.TemporaryDirectory() as tmp:
+        ck = Path(tmp) / "mmpfn_configC.ckpt"
+        torch.save({"state_dict": {k: torch.from_numpy(v) for k, v in sd.items()}, "config": ckpt_config(cfg)}, ck)
+        clf = MMPFNClassifier(
+            model_path=str(ck), mixer_type="MGM+CAP", mgm_heads=MGM, cap_heads=CAP, features_per_group=2,
+            n_estimators=n_estimators, categorical_features_indices=list(range(N_CAT)),
+            ignore_pretraining_limits=True, inference_precision=torch.float32 if prec_f32 else "auto",
+            inference_config=ModelInterfaceConfig(FINGERPRINT_FEATURE=False,
+                                                  PREPROCESS_TRANSFORMS=[PreprocessorConfig(name="none")]),
+        )
+        X = x.astype(np.float64)
+        labels = y.astype(np.int64)
+        clf.fit(X[:N_TRAIN], image[:N_TRAIN], labels[:N_TRAIN])
+    Xq, imq = X[N_TRAIN:], image[N_TRAIN:]
+    clf.predict_proba(Xq, imq)  # warm-up (engine build, weight upload)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        proba = clf.predict_proba(Xq, imq)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    assert np.isfinite(proba).all()
+    return {
+        "value": round(n_estimators * S_ROWS * steps / dt, 1),
+        "unit": "rows/s",
+        "ms_per_predict": round(dt / steps * 1e3, 3),
+        "members": n_estimators,
+        "note": "MMPFNClassifier.predict_proba on host numpy inputs: validation + per-member host transform, "
+                "H2D copies, mixer, member forwards, aggregation, D2H (PCIe-inclusive; not the headline value)",
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -213,6 +263,12 @@ def main():
     rows = M * S_ROWS * args.steps
     value = rows / dt
 
+    api = None
+    if args.api_steps > 0:
+        try:
+            api = api_end_to_end(cfg, sd, x, y, image, M, prec == _lib.PREC_F32, args.api_steps, world)
+        except Exception as e:  # noqa: BLE001 - reported, the headline number stands on its own
+            api = {"error": f"{type(e).__name__}: {e}"}
     roof = time_item_attention(eng, T, args.attn_reps) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -242,6 +298,7 @@ def main():
             },
             "roofline": roof,
             "cpu_baseline": cpu,
+            "api_end_to_end": api,
         }
         print(json.dumps(line))
     if world > 1:

@@ -1,0 +1,165 @@
+"""Inference engines of the classifier: how ensemble members reach the HIP forward.
+
+Mirror of ``mmpfn/models/mmpfn/inference.py``.  ``InferenceEngineCachePreprocessing``
+(``fit_mode="fit_preprocessors"``, the default and the path of ``run.py``) fits
+each member's preprocessing at ``fit`` and at ``predict`` transforms the test
+rows and runs one forward per member (``inference.py:217-351``);
+``InferenceEngineOnDemand`` (``"low_memory"``) re-fits the preprocessing at every
+predict (``:73-213``).
+
+MI355X-specific: the modality projection (MGM / CAP / MoE) depends only on the
+image rows, which every member shares, so it runs once per predict instead of
+once per member (the reference recomputes it inside every forward); members are
+queued back-to-back on the engine's stream with one NaN-status check at the end;
+with ``torch.distributed`` initialised and more than one rank, members are split
+across ranks (longest-processing-time) and the logits all-gathered (RCCL).
+"""
+
+from __future__ import annotations
+
+from collections.abc import Iterator, Sequence
+from dataclasses import dataclass, field
+from typing import Any, Literal
+
+import numpy as np
+import torch
+
+from multimodalpfn_amd import _lib
+from multimodalpfn_amd.preprocessing import fit_preprocessing
+from multimodalpfn_amd.utils import infer_random_state
+
+
+def _precision(model, device: torch.device, autocast: bool, forced: torch.dtype | None) -> int:
+    if forced is not None:
+        return _lib.PREC_F32 if forced in (torch.float32, torch.float64) else _lib.PREC_BF16
+    return _lib.PREC_BF16 if (autocast and device.type == "cuda") else _lib.PREC_F32
+
+
+def _mixer_tokens(model, eng, image_train, image_test, prec: int):
+    """Shared modality tokens of all members (``transformer.py:560-600``), or None."""
+    if image_train is None or image_test is None or model.mixer_type not in ("MGM", "MGM+CAP", "MoE"):
+        return None
+    img = np.concatenate([np.asarray(image_train, dtype=np.float32), np.asarray(image_test, dtype=np.float32)], 0)
+    return eng.mixer_tokens(torch.from_numpy(img), prec)
+
+
+@dataclass
+class _Member:
+    config: Any
+    preprocessor: Any
+    X_train: np.ndarray | None
+    y_train: np.ndarray
+    cat_ix: list[int] | None
+
+
+@dataclass
+class InferenceEngine:
+    """Base: ``iter_outputs`` yields ``(logits [Q, n_out], member config)`` per member."""
+
+    save_peak_mem: bool | Literal["auto"] | float | int
+    dtype_byte_size: int
+
+    def iter_outputs(self, X, image_test, *, device: torch.device, autocast: bool) -> Iterator[tuple]:
+        raise NotImplementedError
+
+    # -- shared member loop -------------------------------------------------------
+    def _run_members(self, members: Sequence[_Member], X, image_train, image_test, *, device, autocast,
+                     forced_dtype, model) -> list[torch.Tensor]:
+        from multimodalpfn_amd.parallel import member_shard
+
+        eng = model.engine(model._device() if device.type != "cuda" else device)
+        prec = _precision(model, eng.device, autocast, forced_dtype)
+        mine, gather = member_shard(len(members), [self._member_cost(m, X, image_test) for m in members])
+        tokens = _mixer_tokens(model, eng, image_train, image_test, prec) if mine else None
+        outs: dict[int, torch.Tensor] = {}
+        for i in mine:
+            m = members[i]
+            if m.X_train is not None:
+                X_test = m.preprocessor.transform(X).X
+                x_full = np.concatenate([np.asarray(m.X_train, np.float32), np.asarray(X_test, np.float32)], 0)
+            else:
+                x_full = None
+            outs[i] = eng.forward(None if x_full is None else torch.from_numpy(x_full), tokens,
+                                  np.asarray(m.y_train, np.float32), prec, check_nan=False)
+        if mine:
+            eng.status()  # NaN / HIP errors of every queued member (transformer.py:727-731,790-796)
+        Q = len(X) if X is not None else len(image_test)
+        return gather(outs, eng.device, Q, model.cfg.n_out)
+
+    @staticmethod
+    def _member_cost(m: _Member, X, image_test) -> float:
+        n_tr = len(m.y_train)
+        n_te = len(X) if X is not None else len(image_test)
+        F = 0 if m.X_train is None else np.asarray(m.X_train).shape[1]
+        return float((F // 2 + 2) * (n_tr + n_te) * n_tr)
+
+
+@dataclass
+class InferenceEngineCachePreprocessing(InferenceEngine):
+    """Preprocessing fitted at ``fit``; one forward per member at predict (``inference.py:217-351``)."""
+
+    X_trains: Sequence[np.ndarray | None] = ()
+    y_trains: Sequence[np.ndarray] = ()
+    image_train: np.ndarray | None = None
+    cat_ixs: Sequence[list[int] | None] = ()
+    ensemble_configs: Sequence[Any] = ()
+    preprocessors: Sequence[Any] = ()
+    model: Any = None
+    force_inference_dtype: torch.dtype | None = None
+
+    @classmethod
+    def prepare(cls, X_train, y_train, image_train, *, cat_ix, model, ensemble_configs, n_workers, rng,
+                dtype_byte_size, force_inference_dtype, save_peak_mem) -> InferenceEngineCachePreprocessing:
+        itr = fit_preprocessing(configs=ensemble_configs, X_train=X_train, y_train=y_train, random_state=rng,
+                                cat_ix=cat_ix, n_workers=n_workers, parallel_mode="block")
+        configs, preprocessors, X_trains, y_trains, cat_ixs = list(zip(*itr))
+        return cls(save_peak_mem=save_peak_mem, dtype_byte_size=dtype_byte_size, X_trains=X_trains,
+                   y_trains=y_trains, image_train=image_train, cat_ixs=cat_ixs, ensemble_configs=configs,
+                   preprocessors=preprocessors, model=model, force_inference_dtype=force_inference_dtype)
+
+    def members(self) -> list[_Member]:
+        return [_Member(c, p, xt, yt, ci) for c, p, xt, yt, ci in
+                zip(self.ensemble_configs, self.preprocessors, self.X_trains, self.y_trains, self.cat_ixs)]
+
+    def iter_outputs(self, X, image_test, *, device: torch.device, autocast: bool) -> Iterator[tuple]:
+        self.model = self.model.to(device)
+        outs = self._run_members(self.members(), X, self.image_train, image_test, device=device,
+                                 autocast=autocast, forced_dtype=self.force_inference_dtype, model=self.model)
+        for out, cfg in zip(outs, self.ensemble_configs):
+            yield out, cfg
+
+
+@dataclass
+class InferenceEngineOnDemand(InferenceEngine):
+    """Nothing cached: members' preprocessing re-fitted at every predict (``inference.py:73-213``)."""
+
+    X_train: np.ndarray | None = None
+    y_train: np.ndarray | None = None
+    image_train: np.ndarray | None = None
+    ensemble_configs: Sequence[Any] = ()
+    cat_ix: list[int] = field(default_factory=list)
+    static_seed: int = 0
+    n_workers: int = 1
+    model: Any = None
+    force_inference_dtype: torch.dtype | None = None
+
+    @classmethod
+    def prepare(cls, X_train, y_train, image_train=None, *, cat_ix, model, ensemble_configs, rng, n_workers,
+                dtype_byte_size, force_inference_dtype, save_peak_mem) -> InferenceEngineOnDemand:
+        static_seed = rng.integers(0, 2**31)  # fixed once so every predict re-fits identically
+        return cls(save_peak_mem=save_peak_mem, dtype_byte_size=dtype_byte_size, X_train=X_train, y_train=y_train,
+                   image_train=image_train, ensemble_configs=ensemble_configs, cat_ix=cat_ix,
+                   static_seed=static_seed, n_workers=n_workers, model=model,
+                   force_inference_dtype=force_inference_dtype)
+
+    def iter_outputs(self, X, image_test, *, device: torch.device, autocast: bool) -> Iterator[tuple]:
+        _, rng = infer_random_state(self.static_seed)
+        itr = fit_preprocessing(configs=self.ensemble_configs, X_train=self.X_train, y_train=self.y_train,
+                                random_state=rng, cat_ix=self.cat_ix, n_workers=self.n_workers,
+                                parallel_mode="in-order")
+        members = [_Member(c, p, xt, yt, ci) for c, p, xt, yt, ci in itr]
+        self.model = self.model.to(device)
+        outs = self._run_members(members, X, self.image_train, image_test, device=device, autocast=autocast,
+                                 forced_dtype=self.force_inference_dtype, model=self.model)
+        for out, m in zip(outs, members):
+            yield out, m.config

@@ -210,7 +210,10 @@ class PerFeatureTransformer(nn.Module):
         steps += [
             NanHandlingEncoderStep(True),
             VariableNumFeaturesEncoderStep(nf, normalize_by_used_features=False),
-            InputNormalizationEncoderStep(),
+            InputNormalizationEncoderStep(
+                remove_outliers=cfg.remove_outliers_sigma is not None,
+                remove_outliers_sigma=cfg.remove_outliers_sigma if cfg.remove_outliers_sigma is not None else 4.0,
+            ),
             VariableNumFeaturesEncoderStep(nf, normalize_by_used_features=True),
             LinearInputEncoderStep(2 * nf, E, bias=False),
         ]

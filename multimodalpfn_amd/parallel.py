@@ -57,3 +57,30 @@ def allgather_logits(local: torch.Tensor, assignment: list[list[int]], rank: int
         if ids:
             out[torch.as_tensor(ids, device=local.device, dtype=torch.long)] = gathered[r * m_max : r * m_max + len(ids)]
     return out
+
+
+def member_shard(n_members: int, costs: list[float], group=None):
+    """This rank's members and a gather function for the classifier's member loop.
+
+    Returns ``(mine, gather)``: ``mine`` lists the member indices this rank runs;
+    ``gather(outs, device, Q, n_out)`` takes ``{member: logits [Q, n_out]}`` of this
+    rank and returns every member's logits in member order, on every rank (one
+    all-gather when ``torch.distributed`` runs more than one rank, else a reorder).
+    """
+    import torch.distributed as dist
+
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    world = dist.get_world_size(group) if multi else 1
+    rank = dist.get_rank(group) if multi else 0
+    assignment = lpt_assign(costs, world) if multi else [list(range(n_members))]
+    mine = assignment[rank]
+
+    def gather(outs: dict[int, torch.Tensor], device, Q: int, n_out: int) -> list[torch.Tensor]:
+        if not multi:
+            return [outs[i] for i in range(n_members)]
+        local = (torch.stack([outs[i] for i in mine]) if mine
+                 else torch.zeros((0, Q, n_out), device=device, dtype=torch.float32))
+        full = allgather_logits(local, assignment, rank, group)
+        return [full[i] for i in range(n_members)]
+
+    return mine, gather

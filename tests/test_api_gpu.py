@@ -1,0 +1,78 @@
+"""End-to-end classifier parity on the GPU against the reference's API-level goldens.
+
+Same checkpoint, data and interface config as ``make_api_golden.py``; the
+reference ran fit/predict_proba on CPU in fp32.  fp32 mode (forced
+``inference_precision=torch.float32``) must reproduce every member's logits to
+1e-4 relative and the ensemble probabilities to 1e-5 absolute; the bf16 mode
+(the default "auto" on a GPU) is held to a loose band and argmax agreement.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from test_api_host import HERE, NAMES, _case, case_data, make_classifier, write_ckpt
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_RTOL = 1e-4
+PROBA_ATOL = 1e-5
+
+
+def _spy(clf):
+    captured = []
+    orig = clf.executor_.iter_outputs
+
+    def spy(*a, **k):
+        for out, c in orig(*a, **k):
+            captured.append(out.detach().float().cpu().numpy())
+            yield out, c
+
+    clf.executor_.iter_outputs = spy
+    return captured
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_predict_proba_fp32_matches_reference(name, tmp_path):
+    case = _case(name)
+    z = np.load(HERE / "golden" / f"api_{name}.npz")
+    d = case_data(case)
+    clf = make_classifier(case, write_ckpt(case, tmp_path), inference_precision=torch.float32)
+    clf.fit(d["X_train"], d["image_train"], d["y_train"])
+    got = _spy(clf)
+    proba = clf.predict_proba(d["X_test"], d["image_test"])
+    for m, lg in enumerate(got):
+        ref = z[f"m{m}_logits"]
+        err = np.abs(lg - ref).max() / max(np.abs(ref).max(), 1e-6)
+        assert err < LOGIT_RTOL, (m, err)
+    np.testing.assert_allclose(proba, z["proba"], atol=PROBA_ATOL, rtol=0)
+    np.testing.assert_array_equal(clf.predict(d["X_test"], d["image_test"]), z["pred"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_predict_proba_bf16_close(name, tmp_path):
+    case = _case(name)
+    z = np.load(HERE / "golden" / f"api_{name}.npz")
+    d = case_data(case)
+    clf = make_classifier(case, write_ckpt(case, tmp_path))  # "auto" -> autocast -> bf16 engine mode
+    clf.fit(d["X_train"], d["image_train"], d["y_train"])
+    assert clf.use_autocast_
+    proba = clf.predict_proba(d["X_test"], d["image_test"])
+    assert np.abs(proba - z["proba"]).max() < 5e-2
+    agree = (proba.argmax(1) == z["proba"].argmax(1)).mean()
+    assert agree >= 0.9, agree
+
+
+def test_low_memory_mode_is_reproducible(tmp_path):
+    """``low_memory`` re-fits members at every predict from one fixed seed (inference.py:148)."""
+    case = _case("pad_none")
+    d = case_data(case)
+    clf = make_classifier(case, write_ckpt(case, tmp_path), inference_precision=torch.float32,
+                          fit_mode="low_memory")
+    clf.fit(d["X_train"], d["image_train"], d["y_train"])
+    a = clf.predict_proba(d["X_test"], d["image_test"])
+    b = clf.predict_proba(d["X_test"], d["image_test"])
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_allclose(a.sum(1), 1.0, atol=1e-6)

@@ -1,0 +1,148 @@
+"""Host side of the classifier against the reference's API-level goldens (CPU).
+
+``tests/golden/api_*.npz`` hold, per ensemble member, what the reference
+``MMPFNClassifier.fit`` produced (``make_api_golden.py``): preprocessed train /
+test tables, permuted labels, categorical indices, class permutation, feature
+shift.  Here the same checkpoint and data go through this package's ``fit``
+(host work only, no GPU needed) and every member must match exactly.
+"""
+
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE / "golden"))
+
+from api_cases import CASES, case_data, ckpt_config  # noqa: E402
+from synth import synth_state_dict  # noqa: E402
+
+from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec  # noqa: E402
+
+NAMES = [c["name"] for c in CASES]
+
+
+def _case(name):
+    return next(c for c in CASES if c["name"] == name)
+
+
+def write_ckpt(case, tmp: Path) -> Path:
+    cfg = ModelConfig(**case["model"])
+    sd = synth_state_dict(state_dict_spec(cfg), case["wseed"])
+    p = tmp / f"{case['name']}.ckpt"
+    torch.save({"state_dict": {k: torch.from_numpy(v) for k, v in sd.items()}, "config": ckpt_config(cfg)}, p)
+    return p
+
+
+def make_classifier(case, ckpt: Path, **over):
+    from multimodalpfn_amd import MMPFNClassifier
+    from multimodalpfn_amd.constants import ModelInterfaceConfig
+    from multimodalpfn_amd.preprocessing import PreprocessorConfig
+
+    ic = dict(case.get("interface", {}))
+    if "PREPROCESS_TRANSFORMS" in ic:
+        ic["PREPROCESS_TRANSFORMS"] = [PreprocessorConfig(**p) for p in ic["PREPROCESS_TRANSFORMS"]]
+    kw = dict(case["clf"]) | over
+    return MMPFNClassifier(model_path=str(ckpt), inference_config=ModelInterfaceConfig(**ic) if ic else None, **kw)
+
+
+def _eq(a, b, what):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    if a.dtype.kind == "f" or b.dtype.kind == "f":
+        np.testing.assert_allclose(a.astype(np.float64), b.astype(np.float64), rtol=1e-12, atol=1e-12,
+                                   equal_nan=True, err_msg=what)
+    else:
+        np.testing.assert_array_equal(a, b, err_msg=what)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_fit_members_match_reference(name, tmp_path):
+    case = _case(name)
+    z = np.load(HERE / "golden" / f"api_{name}.npz")
+    d = case_data(case)
+    clf = make_classifier(case, write_ckpt(case, tmp_path), device="cpu")
+    clf.fit(d["X_train"], d["image_train"], d["y_train"])
+    _eq(clf.classes_, z["classes"], "classes_")
+    _eq(clf.inferred_categorical_indices_, z["inferred_cat"], "inferred categorical")
+    ex = clf.executor_
+    n = len(ex.ensemble_configs)
+    assert n == case["clf"]["n_estimators"]
+    for m, c in enumerate(ex.ensemble_configs):
+        assert str(c.preprocess_config) == str(z[f"m{m}_pp"]), m
+        assert int(c.feature_shift_count) == int(z[f"m{m}_feature_shift"]), m
+        if f"m{m}_class_perm" in z:
+            _eq(c.class_permutation, z[f"m{m}_class_perm"], f"m{m} class perm")
+        else:
+            assert c.class_permutation is None
+        if f"m{m}_subsample" in z:
+            _eq(c.subsample_ix, z[f"m{m}_subsample"], f"m{m} subsample")
+        _eq(ex.y_trains[m], z[f"m{m}_y_train"], f"m{m} y_train")
+        if f"m{m}_X_train" in z:
+            _eq(ex.X_trains[m], z[f"m{m}_X_train"], f"m{m} X_train")
+            _eq(ex.cat_ixs[m], z[f"m{m}_cat_ix"], f"m{m} cat_ix")
+            from multimodalpfn_amd.utils import _fix_dtypes
+
+            X_enc = clf.preprocessor_.transform(_fix_dtypes(d["X_test"], cat_indices=clf.categorical_features_indices))
+            _eq(ex.preprocessors[m].transform(X_enc).X, z[f"m{m}_X_test"], f"m{m} X_test")
+        else:
+            assert ex.X_trains[m] is None
+
+
+def test_fingerprint_matches_python_hash_seed0():
+    """The vectorised SipHash equals CPython's ``hash(bytes)`` under PYTHONHASHSEED=0."""
+    import os
+    import subprocess
+
+    from multimodalpfn_amd.model._siphash import siphash24_rows
+
+    rows = np.random.default_rng(3).standard_normal((6, 5))
+    rows[2] = rows[1]
+    odd = np.frombuffer(b"abcdefghijklmnopqrstu", dtype=np.uint8).reshape(3, 7)
+    code = (
+        "import numpy as np,sys;"
+        "r=np.random.default_rng(3).standard_normal((6,5));r[2]=r[1];"
+        "o=np.frombuffer(b'abcdefghijklmnopqrstu',dtype=np.uint8).reshape(3,7);"
+        "print(' '.join(str(hash(x.tobytes())) for x in list(r)+list(o)))"
+    )
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, PYTHONHASHSEED="0"),
+                         capture_output=True, text=True, check=True).stdout.split()
+    mine = list(siphash24_rows(rows)) + list(siphash24_rows(odd))
+    assert [int(v) for v in mine] == [int(v) for v in out]
+
+
+def test_interface_config_from_user_input():
+    from multimodalpfn_amd.constants import ModelInterfaceConfig
+
+    c = ModelInterfaceConfig.from_user_input(inference_config={"FINGERPRINT_FEATURE": False})
+    assert c.FINGERPRINT_FEATURE is False and c.OUTLIER_REMOVAL_STD == "auto"
+    with pytest.raises(ValueError, match="Unknown kwarg"):
+        ModelInterfaceConfig.from_user_input(inference_config={"NOPE": 1})
+
+
+def test_checkpoint_missing_weight_is_an_error(tmp_path):
+    from multimodalpfn_amd.model.loading import load_model
+
+    case = _case("pad_none")
+    p = write_ckpt(case, tmp_path)
+    ck = torch.load(p, weights_only=True)
+    del ck["state_dict"]["cap.queries"]
+    torch.save(ck, p)
+    with pytest.raises(ValueError, match="cap.queries"):
+        load_model(path=p, model_seed=0, mixer_type="MGM+CAP", mgm_heads=4, cap_heads=2, features_per_group=2)
+
+
+def test_predict_without_gpu_fails_loudly(tmp_path):
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    case = _case("pad_none")
+    d = case_data(case)
+    clf = make_classifier(case, write_ckpt(case, tmp_path))
+    clf.fit(d["X_train"], d["image_train"], d["y_train"])
+    with pytest.raises(RuntimeError, match="no ROCm GPU"):
+        clf.predict_proba(d["X_test"], d["image_test"])

@@ -64,3 +64,33 @@ def test_allgather_single_process_reorders():
     local = torch.stack([torch.full((2, 3), float(m)) for m in a[0]])
     out = allgather_logits(local, a, 0)
     assert [out[i, 0, 0].item() for i in range(3)] == [0.0, 1.0, 2.0]
+
+
+def _shard_worker(rank, world, port, n_members, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from multimodalpfn_amd.parallel import member_shard
+
+    mine, gather = member_shard(n_members, [float(1 + i % 3) for i in range(n_members)])
+    outs = {i: torch.full((4, 10), float(i)) for i in mine}
+    full = gather(outs, torch.device("cpu"), 4, 10)
+    ok = len(full) == n_members and all(torch.all(full[i] == float(i)).item() for i in range(n_members))
+    q.put((rank, ok, mine))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_members", [5, 1])
+def test_member_shard_gloo_world2(n_members):
+    """The classifier's member loop split over 2 ranks returns every member on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, n_members, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert sorted(i for _, _, mine in res for i in mine) == list(range(n_members))
