@@ -88,8 +88,6 @@ def create_inference_engine(
     if fit_mode == "fit_preprocessors":
         return InferenceEngineCachePreprocessing.prepare(X_train, y_train, image_train, **common)
     if fit_mode == "fit_with_cache":
-        from multimodalpfn_amd.inference import InferenceEngineCacheKV
-
-        return InferenceEngineCacheKV.prepare(X_train, y_train, image_train, device=device_, autocast=use_autocast_,
-                                              **common)
+        raise NotImplementedError("fit_mode='fit_with_cache' (train-KV cache) is not served yet; "
+                                  "use 'fit_preprocessors'")
     raise ValueError(f"Invalid fit_mode: {fit_mode}")
