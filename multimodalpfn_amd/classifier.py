@@ -151,6 +151,7 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
             X = enc.fit_transform(X)
             assert isinstance(X, np.ndarray)
             self.preprocessor_ = enc
+            self._plan_ordinal()
             ic = self.interface_config_
             self.inferred_categorical_indices_ = infer_categorical_features(
                 X=X,
@@ -200,6 +201,57 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
         return self
 
     # ------------------------------------------------------------------ predict
+    def _encode_predict_X(self, X) -> np.ndarray:
+        """validate -> _fix_dtypes -> fitted ordinal encoder (``classifier.py:529-532``).
+
+        A plain numeric ndarray (the run.py case) takes a numpy path computing the same
+        table as the pandas / ColumnTransformer route in ~1/20 of its time: categorical
+        columns map to their index in the fitted sorted categories (unseen -> -1,
+        missing -> NaN), encoded columns first, then the remainder in order
+        (``tests/test_api_host.py`` checks the two routes agree).
+        """
+        X = validate_X_predict(X, self)
+        fast = getattr(self, "_ordinal_plan_", None)
+        if fast is not None and isinstance(X, np.ndarray) and X.dtype.kind in "biuf" and X.ndim == 2:
+            Xf = X.astype(np.float64, copy=False)
+            cols, cats, nan_seen, rem = fast
+            out = np.empty((Xf.shape[0], len(cols) + len(rem)), dtype=np.float64)
+            for k, (j, c) in enumerate(zip(cols, cats)):
+                v = Xf[:, j]
+                idx = np.searchsorted(c, v)
+                idc = np.minimum(idx, max(len(c) - 1, 0))
+                hit = (idx < len(c)) & (c[idc] == v) if len(c) else np.zeros(v.shape, bool)
+                # missing -> NaN only if missing was a fitted category, else it is unseen (-1)
+                miss = np.nan if nan_seen[k] else -1.0
+                out[:, k] = np.where(np.isnan(v), miss, np.where(hit, idx, -1.0))
+            if rem:
+                out[:, len(cols):] = Xf[:, rem]
+            return out
+        X = _fix_dtypes(X, cat_indices=self.categorical_features_indices)
+        return self.preprocessor_.transform(X)
+
+    def _plan_ordinal(self) -> None:
+        """Record the fitted encoder's column plan for the numpy predict path (or None)."""
+        self._ordinal_plan_ = None
+        enc = self.preprocessor_
+        ts = [(n, t, c) for n, t, c in enc.transformers_ if not (n == "remainder" and t == "drop")]
+        if not ts or ts[0][0] != "encoder" or any(n not in ("encoder", "remainder") for n, _, _ in ts):
+            return
+        cols = [int(c) for c in ts[0][2]]
+        oe = ts[0][1]
+        if len(cols) and not hasattr(oe, "categories_"):
+            return
+        cats, nan_seen = [], []
+        for c in (oe.categories_ if len(cols) else []):
+            c = np.asarray(c)
+            if c.dtype.kind not in "biuf":
+                return
+            c = c.astype(np.float64)
+            nan_seen.append(bool(np.isnan(c).any()))
+            cats.append(np.sort(c[~np.isnan(c)]))
+        rem = [int(c) for c in ts[1][2]] if len(ts) > 1 else []
+        self._ordinal_plan_ = (cols, cats, nan_seen, rem)
+
     def predict(self, X, X_image: np.ndarray | None) -> np.ndarray:
         """Arg-max class labels (``classifier.py:504-515``)."""
         proba = self.predict_proba(X, X_image)
@@ -209,9 +261,7 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
         """Class probabilities ``[Q, n_classes]`` fp32 left on the GPU (no rounding)."""
         check_is_fitted(self)
         if X is not None:
-            X = validate_X_predict(X, self)
-            X = _fix_dtypes(X, cat_indices=self.categorical_features_indices)
-            X = self.preprocessor_.transform(X)
+            X = self._encode_predict_X(X)
         logits, perms = [], []
         for out, config in self.executor_.iter_outputs(X, image_test=image_test, device=self.device_,
                                                        autocast=self.use_autocast_):

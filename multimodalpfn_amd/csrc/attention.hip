@@ -60,7 +60,21 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   constexpr int NT = 64 * NW;  // threads per block
-  const int h = blockIdx.y, b = blockIdx.z;
+  // XCD-aware block order: the hardware deals consecutive workgroups round-robin to the 8
+  // XCDs; remap so each XCD works through a contiguous run of (query block, head, batch)
+  // ids, i.e. the blocks sharing one K/V sequence share that XCD's L2.
+  int qblk, h, b;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int nb = gx * gy * gridDim.z;
+    const int pid = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int xcd = pid & 7, slot = pid >> 3;
+    const int lid = xcd * (nb >> 3) + min(xcd, nb & 7) + slot;
+    qblk = lid % gx;
+    const int rest = lid / gx;
+    h = rest % gy;
+    b = rest / gy;
+  }
   const int kvh = p.kvh_fixed >= 0 ? p.kvh_fixed : h;
   const int s0 = p.s0, nq = p.nq, nk = p.nk, Npad = p.kpad;
   const TE* Q = (const TE*)p.q + b * p.q_bstride + h * p.q_hstride;
@@ -68,7 +82,7 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
   const TE* Vg = (const TE*)p.vt + b * p.kv_bstride + kvh * p.kv_hstride;
   const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
 
-  const int qi = blockIdx.x * (32 * NW) + wave * 32 + r;  // query offset in [0, nq)
+  const int qi = qblk * (32 * NW) + wave * 32 + r;  // query offset in [0, nq)
   const int64_t qs = s0 + min(qi, nq - 1);
 
   // ---- Q fragments (B operand of S^T = K Q^T), pre-scaled by c
@@ -174,14 +188,27 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
 
     // ---- S^T - m_ref for the two 32-key subtiles
     f32x16 sacc[2];
+    if constexpr (BF16) {
+      // all four K fragments in flight before the first MFMA (the scheduler otherwise
+      // serialises read -> wait -> MFMA and exposes the LDS latency four times)
+      bf16x8 kf[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const unsigned char* krow = Ks + (32 * u + r) * L::KROW;
+        kf[u][0] = *(const bf16x8*)(krow + (8 * hh) * 2);
+        kf[u][1] = *(const bf16x8*)(krow + (16 + 8 * hh) * 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qb[0], negm, 0, 0, 0);
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][1], qb[1], sacc[u], 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const unsigned char* krow = Ks + (32 * u + r) * L::KROW;
       if constexpr (BF16) {
-        const bf16x8 k0f = *(const bf16x8*)(krow + (8 * hh) * 2);
-        const bf16x8 k1f = *(const bf16x8*)(krow + (16 + 8 * hh) * 2);
-        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0f, qb[0], negm, 0, 0, 0);
-        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1f, qb[1], sacc[u], 0, 0, 0);
       } else {
         float kf[16];
 #pragma unroll

@@ -133,6 +133,20 @@ std::vector<float> transpose_out(const std::vector<float>& w, int HD, int E) {
   return o;
 }
 
+// W2 [E][Fh] with each 32-wide hidden group permuted for mlp_rows_kernel's K order:
+// position 8g + j holds hidden 4g + j (j < 4) or 16 + 4g + (j - 4) (j >= 4)
+std::vector<float> pack_mlp2_perm(const std::vector<float>& w, int E, int Fh) {
+  std::vector<float> o(w.size());
+  for (int e = 0; e < E; ++e)
+    for (int c = 0; c < Fh; c += 32)
+      for (int pos = 0; pos < 32; ++pos) {
+        const int g = pos >> 3, j = pos & 7;
+        const int hid = j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4);
+        o[(size_t)e * Fh + c + pos] = w[(size_t)e * Fh + c + hid];
+      }
+  return o;
+}
+
 int up2(mmpfn_ctx* ctx, DevBuf& f, DevBuf& h, const std::vector<float>& v) {
   int rc = upload(ctx, f, v, false);
   if (rc) return rc;
@@ -168,7 +182,8 @@ int finalize(mmpfn_ctx* ctx) {
     if ((rc = up2(ctx, L.feat_out, L.feat_out_h, transpose_out(*fo, HD, E)))) return rc;
     if ((rc = up2(ctx, L.item_out, L.item_out_h, transpose_out(*io, HD, E)))) return rc;
     if ((rc = up2(ctx, L.mlp1, L.mlp1_h, *m1))) return rc;
-    if ((rc = up2(ctx, L.mlp2, L.mlp2_h, *m2))) return rc;
+    if ((rc = upload(ctx, L.mlp2, *m2, false))) return rc;
+    if ((rc = upload(ctx, L.mlp2_h, pack_mlp2_perm(*m2, E, Fh), true))) return rc;
     std::vector<float> wtrain((size_t)3 * HD * E), wtest((size_t)HD * E);
     if (d.two_sets_of_queries) {
       GETW(wq, p + "self_attn_between_items._w_q", (size_t)2 * HD * E);
@@ -402,7 +417,10 @@ int run_layer(mmpfn_ctx* ctx, int l) {
   unsigned char* big = (unsigned char*)ctx->ws_big.p;
 
   // ---- attention between features (layer.py:332-339): batch = row s, T tokens
-  {
+  if (bf && d.nhead * 32 == E && feat_block_rows(T) > 0) {
+    // one fused kernel: QKV, per-row attention, out-projection, residual + LN out of LDS
+    HIPCHK(launch_feat_block(X, L.feat_qkv_h.p, L.feat_out_h.p, S, T, E, H, d.ln_eps, st));
+  } else {
     const int Tpad = (T + 63) / 64 * 64;
     void* Qf = big;
     void* Kf = big + (size_t)R * E * eb;
@@ -452,7 +470,10 @@ int run_layer(mmpfn_ctx* ctx, int l) {
     HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
   }
   // ---- MLP (mlp.py:93-104), fused up/GELU/down/residual/LN
-  HIPCHK(launch_mlp_fused(X, W(L.mlp1, L.mlp1_h, prec), W(L.mlp2, L.mlp2_h, prec), R, E, d.nhid, d.ln_eps, prec, st));
+  if (bf && d.nhid % 32 == 0)  // W2 bf16 copy is stored in mlp_rows_kernel's permuted K order
+    HIPCHK(launch_mlp_rows(X, L.mlp1_h.p, L.mlp2_h.p, R, E, d.nhid, d.ln_eps, st));
+  else
+    HIPCHK(launch_mlp_fused(X, L.mlp1.p, L.mlp2.p, R, E, d.nhid, d.ln_eps, PREC_F32, st));
   return MMPFN_OK;
 }
 

@@ -23,7 +23,7 @@ namespace {
 
 constexpr int BM = 64;
 constexpr int BN = 192;
-constexpr int ROWB = 144;  // LDS bytes per staged row: 128 data + 16 pad (conflict-free b128 reads)
+constexpr int ROWB = 160;  // LDS bytes per staged row: 128 data + 32 pad (32 mod 64: conflict-free ds_read_b128)
 constexpr int LDS_STAGE = (BM + BN) * ROWB;
 constexpr int LN_STRIDE = 196;  // floats per row of the LayerNorm epilogue buffer
 constexpr int LDS_LN = BM * LN_STRIDE * 4;

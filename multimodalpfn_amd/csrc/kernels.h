@@ -54,6 +54,17 @@ hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool ou
 hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M, int E, int Fh, float eps, int prec,
                             hipStream_t st);
 
+// row-resident MLP sublayer (bf16 only): W1 [Fh][E] bf16, W2 [E][Fh] bf16 in the permuted
+// hidden order of pack_mlp2_perm (capi.cpp); Fh % 32 == 0
+hipError_t launch_mlp_rows(float* X, const void* W1, const void* W2perm, int64_t M, int E, int Fh, float eps,
+                           hipStream_t st);
+
+// fused attention-between-features sublayer (bf16 only): X <- LN(X + MHA_feat(X)) per row,
+// wqkv [3*H*32][E] bf16, wout [E][H*32] bf16; rows per block = feat_block_rows(T) (0: unsupported T)
+int feat_block_rows(int T);
+hipError_t launch_feat_block(float* X, const void* wqkv, const void* wout, int S, int T, int E, int H, float eps,
+                             hipStream_t st);
+
 // ---- attention -------------------------------------------------------------------
 // generic MFMA attention over a batch (blockIdx.z) of independent sequences:
 //   Q  [b][h][pos][32] (row = s0 + q), K [b][kvh][key][32], V^T [b][kvh][32][kpad],

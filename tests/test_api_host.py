@@ -146,3 +146,25 @@ def test_predict_without_gpu_fails_loudly(tmp_path):
     clf.fit(d["X_train"], d["image_train"], d["y_train"])
     with pytest.raises(RuntimeError, match="no ROCm GPU"):
         clf.predict_proba(d["X_test"], d["image_test"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_numpy_predict_encoding_matches_pandas_route(name, tmp_path):
+    """The numpy fast path of predict-time encoding equals _fix_dtypes + ColumnTransformer."""
+    from multimodalpfn_amd.utils import _fix_dtypes, validate_X_predict
+
+    case = _case(name)
+    d = case_data(case)
+    if d["X_train"] is None:
+        pytest.skip("image-only case")
+    clf = make_classifier(case, write_ckpt(case, tmp_path), device="cpu")
+    clf.fit(d["X_train"], d["image_train"], d["y_train"])
+    assert clf._ordinal_plan_ is not None
+    Xt = d["X_test"].copy()
+    g = np.random.default_rng(0)
+    Xt[g.random(Xt.shape) < 0.05] = np.nan  # missing values
+    Xt[0, :] = 97.0  # unseen categories
+    fast = clf._encode_predict_X(Xt)
+    slow = clf.preprocessor_.transform(_fix_dtypes(validate_X_predict(Xt, clf),
+                                                   cat_indices=clf.categorical_features_indices))
+    np.testing.assert_array_equal(fast, np.asarray(slow, dtype=np.float64))

@@ -93,6 +93,32 @@ def test_each_layer_matches_oracle_layer():
         X = got
 
 
+@pytest.mark.parametrize("case", ["tab_small", "mgmcap_edge", "two_queries", "pad_ufes_12l"])
+def test_each_layer_bf16_close_to_oracle_layer(case):
+    """bf16 mode, one layer at a time from the oracle's input (fused feature-block kernel,
+    bf16 item attention, fused MLP): bf16-rounding-level agreement with the fp64 oracle."""
+    from multimodalpfn_amd import _lib
+
+    z, meta, cfg, sd = load_case(case)
+    model = make_model(cfg, sd)
+    eng = model.engine()
+    spec = oracle_spec(cfg)
+    w = torch_sd(sd)
+    tok = None
+    if "image" in z:
+        tok = eng.mixer_tokens(torch.from_numpy(z["image"]).cuda(), _lib.PREC_F32)
+    xin = torch.from_numpy(z["x"]).cuda() if "x" in z else None
+    X = eng.embed_state(xin, tok, z["y_train"], _lib.PREC_BF16).cpu()
+    N = len(z["y_train"])
+    for l in range(min(cfg.nlayers, 3)):
+        ref = layer_forward(spec, w, l, X.double(), N).float()
+        got = eng.run_layers(l, l + 1).cpu()
+        assert torch.isfinite(got).all()
+        err = rel_err(got.numpy(), ref.numpy())
+        assert err < 4e-2, (l, err)
+        X = got
+
+
 def _attn_ref(q, k, v):
     s = (q.double() @ k.double().transpose(-1, -2)) / math.sqrt(q.shape[-1])
     return torch.softmax(s, -1) @ v.double()

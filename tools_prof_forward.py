@@ -1,0 +1,45 @@
+"""Profiling driver: a few bf16 member forwards at the config-C shape (for rocprofv3 --pmc passes).
+
+Usage (on the GPU box):  rocprofv3 --pmc <counters> -d <dir> -o run --output-format csv -- \
+                              python3 tools_prof_forward.py [n_forwards]
+"""
+
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests" / "golden"))
+
+from synth import synth_image, synth_labels, synth_state_dict, synth_table  # noqa: E402
+
+from multimodalpfn_amd import _lib  # noqa: E402
+from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec  # noqa: E402
+from multimodalpfn_amd.model.transformer import PerFeatureTransformer  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    cfg = ModelConfig(mgm_heads=64, cap_heads=24)
+    sd = synth_state_dict(state_dict_spec(cfg), 2)
+    model = PerFeatureTransformer(cfg)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model.to("cuda")
+    eng = model.engine()
+    S, N = 2298, 1838
+    x = torch.from_numpy(synth_table(S, 21, 2, n_cat=18)).cuda()
+    im = torch.from_numpy(synth_image(S, 1, 2)).cuda()
+    y = synth_labels(S, 6, 2)[:N]
+    tok = eng.mixer_tokens(im, _lib.PREC_BF16)
+    for _ in range(n):
+        out = eng.forward(x, tok, y, _lib.PREC_BF16, check_nan=False)
+    eng.status()
+    torch.cuda.synchronize()
+    print("ok", tuple(out.shape), float(out.abs().mean()))
+
+
+if __name__ == "__main__":
+    main()
