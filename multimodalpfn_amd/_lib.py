@@ -78,7 +78,8 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = Path(path) if path is not None else LIB_PATH
+    # MMPFN_LIB: diagnostics only (e.g. the stamps build of `make dbg`)
+    p = Path(path) if path is not None else Path(os.environ.get("MMPFN_LIB", str(LIB_PATH)))
     if not p.exists():
         raise RuntimeError(
             f"MMPFN HIP engine library not found at {p}; build it with "

@@ -449,25 +449,35 @@ int run_layer(mmpfn_ctx* ctx, int l) {
     void* Qi = big;
     void* Ki = big + (size_t)R * E * eb;
     void* Vi = (unsigned char*)Ki + (size_t)T * H * Npad * 32 * eb;
-    GemmArgs a = gargs();
-    a.A = X, a.lda = E, a.a_rdiv = N, a.a_rmul = S, a.a_roff = 0;
-    a.W = W(L.item_qkv, L.item_qkv_h, prec);
-    a.M = T * N, a.N = 3 * E, a.K = E;
-    a.q = Qi, a.k = Ki, a.v = Vi, a.S = S, a.Npad = Npad, a.T = T, a.H = H;
-    HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
-    if (Q > 0) {
-      GemmArgs c = a;
-      c.a_rdiv = Q, c.a_roff = N;
-      c.W = W(L.item_qtest, L.item_qtest_h, prec);
-      c.M = T * Q, c.N = E;
-      HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+    if (bf && E == 192) {  // row-resident projections straight into the attention layouts
+      HIPCHK(launch_rowgemm_qkv(X, N, S, 1, 0, L.item_qkv_h.p, T * N, 3 * E, Qi, Ki, Vi, S, Npad, H, st));
+      if (Q > 0)
+        HIPCHK(launch_rowgemm_qkv(X, Q, S, 1, N, L.item_qtest_h.p, T * Q, E, Qi, Ki, Vi, S, Npad, H, st));
+    } else {
+      GemmArgs a = gargs();
+      a.A = X, a.lda = E, a.a_rdiv = N, a.a_rmul = S, a.a_roff = 0;
+      a.W = W(L.item_qkv, L.item_qkv_h, prec);
+      a.M = T * N, a.N = 3 * E, a.K = E;
+      a.q = Qi, a.k = Ki, a.v = Vi, a.S = S, a.Npad = Npad, a.T = T, a.H = H;
+      HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+      if (Q > 0) {
+        GemmArgs c = a;
+        c.a_rdiv = Q, c.a_roff = N;
+        c.W = W(L.item_qtest, L.item_qtest_h, prec);
+        c.M = T * Q, c.N = E;
+        HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+      }
     }
     HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, T, H, Npad, 0, N, N, -1, prec, st));
     if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, T, H, Npad, N, Q, N, 0, prec, st));
-    GemmArgs b = gargs();
-    b.A = O, b.lda = E, b.W = W(L.item_out, L.item_out_h, prec);
-    b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
-    HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
+    if (bf && E == 192) {
+      HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, R, X, d.ln_eps, st));
+    } else {
+      GemmArgs b = gargs();
+      b.A = O, b.lda = E, b.W = W(L.item_out, L.item_out_h, prec);
+      b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
+      HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
+    }
   }
   // ---- MLP (mlp.py:93-104), fused up/GELU/down/residual/LN
   if (bf && d.nhid % 32 == 0)  // W2 bf16 copy is stored in mlp_rows_kernel's permuted K order

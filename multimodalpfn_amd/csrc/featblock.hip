@@ -48,6 +48,16 @@ struct FbArgs {
   float eps, qscale;
 };
 
+#ifdef MMPFN_STAMPS  // phase timestamps of one block (diagnostics build only: make dbg)
+__device__ unsigned long long g_fb_stamps[32];
+#define FB_STAMP(k) \
+  if (blockIdx.x == gridDim.x / 2 && threadIdx.x == 0) g_fb_stamps[(k)] = __builtin_amdgcn_s_memtime()
+#else
+#define FB_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -88,6 +98,7 @@ __global__ __launch_bounds__(256, 1) void feat_block_kernel(const FbArgs p) {
     }
   };
 
+  FB_STAMP(0);
   // ---- phase 0: token rows -> bf16 A (pad rows zero), head-0 weights, zero the QKV tail.
   // All of a thread's loads are issued before the first use.
   wfetch(0);
@@ -118,6 +129,7 @@ __global__ __launch_bounds__(256, 1) void feat_block_kernel(const FbArgs p) {
   for (int i = tid; i < QTAIL * QST / 8; i += 256) *(u32x4*)(Qs + Mp * QST + i * 8) = u32x4{0u, 0u, 0u, 0u};
   wstash();
   __syncthreads();
+  FB_STAMP(1);
 
   const int nt = (T + 15) >> 4;  // 16-token tiles per row (<= 4)
   for (int h = 0; h < FH; ++h) {
@@ -164,6 +176,7 @@ __global__ __launch_bounds__(256, 1) void feat_block_kernel(const FbArgs p) {
       }
     }
     __syncthreads();
+    FB_STAMP(2 + 3 * h);
     if (h + 1 < FH) wfetch(h + 1);  // lands while this head's attention runs
 
     // ---- attention of each row (one wave per row)
@@ -200,8 +213,7 @@ __global__ __launch_bounds__(256, 1) void feat_block_kernel(const FbArgs p) {
             mx = fmaxf(mx, sc[kt][qt][i]);
           }
         }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx = max_rows4(mx);
         float sum = 0.f;
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) {
@@ -213,8 +225,7 @@ __global__ __launch_bounds__(256, 1) void feat_block_kernel(const FbArgs p) {
             sum += e;
           }
         }
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
+        sum = sum_rows4(sum);
         inv_l[qt] = __builtin_amdgcn_rcpf(sum);
         // P^T as the B operand: K positions 8*fg + j <-> keys 32*ks + 4*fg + j (j < 4),
         // 32*ks + 16 + 4*fg + (j - 4) (j >= 4): exactly this lane's accumulator rows
@@ -271,9 +282,11 @@ __global__ __launch_bounds__(256, 1) void feat_block_kernel(const FbArgs p) {
       }
     }
     __syncthreads();
+    FB_STAMP(3 + 3 * h);
     if (h + 1 < FH) {
       wstash();  // W_h's readers (the QKV phase) finished before the barrier above
       __syncthreads();
+      FB_STAMP(4 + 3 * h);
     }
   }
 
@@ -292,6 +305,7 @@ __global__ __launch_bounds__(256, 1) void feat_block_kernel(const FbArgs p) {
     }
   }
   __syncthreads();
+  FB_STAMP(20);
 
   // ---- out-projection Y^T [E][tokens] = Wout . O^T, wave owns token tiles wave, wave + 4
   f32x4 y[2][12];
@@ -322,6 +336,7 @@ __global__ __launch_bounds__(256, 1) void feat_block_kernel(const FbArgs p) {
     }
   }
 
+  FB_STAMP(21);
   // ---- residual + LayerNorm per token (lane = token, 48 of its 192 features in registers)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -342,8 +357,7 @@ __global__ __launch_bounds__(256, 1) void feat_block_kernel(const FbArgs p) {
         s += y[j][f][i];
       }
     }
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
+    s = sum_rows4(s);
     const float mean = s * (1.0f / FE);
     float q = 0.f;
 #pragma unroll
@@ -353,8 +367,7 @@ __global__ __launch_bounds__(256, 1) void feat_block_kernel(const FbArgs p) {
         const float dl = y[j][f][i] - mean;
         q += dl * dl;
       }
-    q += __shfl_xor(q, 16, 64);
-    q += __shfl_xor(q, 32, 64);
+    q = sum_rows4(q);
     const float inv = 1.0f / sqrtf(q * (1.0f / FE) + p.eps);
     if (valid) {
 #pragma unroll
@@ -374,6 +387,12 @@ size_t feat_block_lds(int mp) {
 }
 
 }  // namespace
+
+#ifdef MMPFN_STAMPS
+extern "C" int mmpfn_dbg_featblock_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fb_stamps), sizeof(g_fb_stamps));
+}
+#endif
 
 int feat_block_rows(int T) { return (T >= 1 && T <= 64) ? MAXTOK / T : 0; }
 

@@ -59,6 +59,16 @@ hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M,
 hipError_t launch_mlp_rows(float* X, const void* W1, const void* W2perm, int64_t M, int E, int Fh, float eps,
                            hipStream_t st);
 
+// row-resident item-attention projections (bf16, K = 192, rowgemm.hip):
+//   QKV: X rows (remap (m/rdiv)*rmul + (m%rdiv)*rmul2 + roff) . W^T, W [N][192] (N = 576 or 192),
+//        scattered to Q [b][h][pos][32], K [b][h][pos][32] (Npad rows), V^T [b][h][32][Npad],
+//        b = m / rdiv, pos = roff + m % rdiv
+//   RES_LN: X <- LN(X + O . W^T), O [M][192] bf16, W [192][192] bf16
+hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
+                              const void* W, int M, int N, void* q, void* k, void* vt, int S, int Npad, int H,
+                              hipStream_t st);
+hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, float* X, float eps, hipStream_t st);
+
 // fused attention-between-features sublayer (bf16 only): X <- LN(X + MHA_feat(X)) per row,
 // wqkv [3*H*32][E] bf16, wout [E][H*32] bf16; rows per block = feat_block_rows(T) (0: unsupported T)
 int feat_block_rows(int T);

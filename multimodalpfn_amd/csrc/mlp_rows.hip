@@ -166,8 +166,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X,
         s += y[o][tt][i];
       }
     }
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
+    s = sum_rows4(s);
     const float mean = s * (1.0f / RE);
     float q = 0.f;
 #pragma unroll
@@ -177,8 +176,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X,
         const float dl = y[o][tt][i] - mean;
         q += dl * dl;
       }
-    q += __shfl_xor(q, 16, 64);
-    q += __shfl_xor(q, 32, 64);
+    q = sum_rows4(q);
     const float inv = 1.0f / sqrtf(q * (1.0f / RE) + eps);
     if (valid) {
 #pragma unroll

@@ -1,0 +1,278 @@
+// Row-resident projection GEMMs of the item-attention sublayer for gfx950 (bf16 mode):
+//   * QKV : rows of X (fp32 state) . W^T (W [N][192], N = 576 q|k|v or 192 q only),
+//           scattered straight into the attention layouts Q [b][h][pos][32],
+//           K [b][h][pos][32] (Npad rows) and V^T [b][h][32][Npad]  (layer.py:341-372);
+//   * RES_LN : X <- LayerNorm(X + O . Wout^T)  (layer.py:437-455, no affine).
+// K is the model width (192): a wave keeps its 32 rows as bf16 fragments in registers
+// for the whole kernel and the block (4 waves, 128 rows) stages one 192 x 192 weight
+// panel at a time in LDS (row stride 416 B: conflict-free ds_read_b128), so each
+// output panel is one barrier and 144 v_mfma_f32_16x16x32_bf16 per wave.  Q and K
+// panels are computed transposed (lane = row, 4 consecutive head dims -> one 8-byte
+// store); the V panel is computed untransposed (lane = head dim, 4 consecutive rows
+// -> one 8-byte store into V^T).  The RES_LN panel keeps Y^T in registers and does the
+// residual + LayerNorm across lanes (in-register permlane reductions).
+#include "common.h"
+#include "kernels.h"
+
+namespace mmpfn {
+
+namespace {
+
+constexpr int GE = 192;         // K (model width) and panel width
+constexpr int GROWS = 128;      // rows per block
+constexpr int WST = GE + 16;    // LDS panel row stride (bf16): 416 B
+constexpr int WPC = GE * GE / 8 / 256;  // 16-B panel pieces per thread (18)
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+struct RgArgs {
+  const void* A;     // fp32 rows (QKV) or bf16 rows (RES_LN), ld = 192
+  int64_t a_rdiv, a_rmul, a_rmul2, a_roff;  // logical row m -> memory row (m/rdiv)*rmul + (m%rdiv)*rmul2 + roff
+  const bf16* W;     // [N][192]
+  int M, N;
+  // QKV scatter: b = m / a_rdiv, pos = a_roff + m % a_rdiv
+  bf16 *q, *k, *vt;
+  int S, Npad, H;
+  // RES_LN
+  float* X;
+  float eps;
+};
+
+template <bool AF32>
+__device__ __forceinline__ void load_rows(const RgArgs& p, int64_t m0, int fr, int fg, bf16x8 (&af)[2][GE / 32]) {
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int m = (int)min(m0 + tt * 16 + fr, (int64_t)p.M - 1);
+    const int rd = (int)p.a_rdiv, mb = m / rd;
+    const int64_t mr = (int64_t)mb * p.a_rmul + (int64_t)(m - mb * rd) * p.a_rmul2 + p.a_roff;
+    if constexpr (AF32) {
+      const float* xr = (const float*)p.A + mr * GE + fg * 8;
+      f32x4 lo[GE / 32], hi[GE / 32];
+#pragma unroll
+      for (int ks = 0; ks < GE / 32; ++ks) {
+        lo[ks] = *(const f32x4*)(xr + ks * 32);
+        hi[ks] = *(const f32x4*)(xr + ks * 32 + 4);
+      }
+#pragma unroll
+      for (int ks = 0; ks < GE / 32; ++ks) {
+        bf16x8 b;
+        b[0] = (bf16)lo[ks][0], b[1] = (bf16)lo[ks][1], b[2] = (bf16)lo[ks][2], b[3] = (bf16)lo[ks][3];
+        b[4] = (bf16)hi[ks][0], b[5] = (bf16)hi[ks][1], b[6] = (bf16)hi[ks][2], b[7] = (bf16)hi[ks][3];
+        af[tt][ks] = b;
+      }
+    } else {
+      const bf16* xr = (const bf16*)p.A + mr * GE + fg * 8;
+#pragma unroll
+      for (int ks = 0; ks < GE / 32; ++ks) af[tt][ks] = *(const bf16x8*)(xr + ks * 32);
+    }
+  }
+}
+
+// stage W rows [n0, n0 + 192) into the LDS panel (all threads; caller brackets with barriers)
+__device__ __forceinline__ void stage_panel(const bf16* W, int n0, bf16* Ws, int tid) {
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {  // two rounds of 9 pieces: bounded register footprint
+    u32x4 r[WPC / 2];
+#pragma unroll
+    for (int j = 0; j < WPC / 2; ++j) {
+      const int i = tid + 256 * (half * (WPC / 2) + j);
+      r[j] = *(const u32x4*)(W + (int64_t)(n0 + i / (GE / 8)) * GE + (i % (GE / 8)) * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < WPC / 2; ++j) {
+      const int i = tid + 256 * (half * (WPC / 2) + j);
+      *(u32x4*)(Ws + (i / (GE / 8)) * WST + (i % (GE / 8)) * 8) = r[j];
+    }
+  }
+}
+
+// acc[f][tt] = panel(f) x rows(tt) over K = 192; TRANS: C^T (features x rows), else C (rows x features)
+template <bool TRANS>
+__device__ __forceinline__ void panel_mma(const bf16* Ws, const bf16x8 (&af)[2][GE / 32], int fr, int fg,
+                                          f32x4 (&acc)[GE / 16][2]) {
+#pragma unroll
+  for (int f = 0; f < GE / 16; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // W fragments in groups of 4 feature tiles, the next group's reads issued before this
+  // group's MFMAs (sched barriers keep the reads early; 2 x 4 fragments in flight)
+  constexpr int NG = GE / 16 / 4;  // groups per k-step (3)
+  bf16x8 w[2][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[0][i] = *(const bf16x8*)(Ws + (i * 16 + fr) * WST + fg * 8);
+#pragma unroll
+  for (int it = 0; it < (GE / 32) * NG; ++it) {
+    const int ks = it / NG, g = it % NG;
+    if (it + 1 < (GE / 32) * NG) {
+      const int ks1 = (it + 1) / NG, g1 = (it + 1) % NG;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        w[(it + 1) & 1][i] = *(const bf16x8*)(Ws + ((g1 * 4 + i) * 16 + fr) * WST + ks1 * 32 + fg * 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        if constexpr (TRANS)
+          acc[g * 4 + i][tt] = mfma16(w[it & 1][i], af[tt][ks], acc[g * 4 + i][tt]);
+        else
+          acc[g * 4 + i][tt] = mfma16(af[tt][ks], w[it & 1][i], acc[g * 4 + i][tt]);
+      }
+  }
+}
+
+// one output panel per block: grid = panels x row tiles, ordered so the panels of one row
+// tile are consecutive ids on one XCD (the rows come from HBM once, then from that L2)
+__global__ __launch_bounds__(256, 2) void rowgemm_qkv_kernel(const RgArgs p, int npanels) {
+  __shared__ __attribute__((aligned(16))) bf16 Ws[GE * WST];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  int j, tile;
+  {
+    const int nb = gridDim.x, pid = blockIdx.x;
+    const int xcd = pid & 7, slot = pid >> 3;
+    const int lid = xcd * (nb >> 3) + min(xcd, nb & 7) + slot;
+    j = lid % npanels;
+    tile = lid / npanels;
+  }
+  const int64_t m0 = (int64_t)tile * GROWS + wave * 32;
+  stage_panel(p.W, j * GE, Ws, tid);
+  bf16x8 af[2][GE / 32];
+  load_rows<true>(p, m0, fr, fg, af);
+  f32x4 acc[GE / 16][2];
+  __syncthreads();
+  {
+    if (j < 2) {
+      panel_mma<true>(Ws, af, fr, fg, acc);
+      // C^T: lane = row m (tile tt, col fr); rows of the tile = features 16f + 4fg + i
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int m = (int)(m0 + tt * 16 + fr);
+        if (m >= p.M) continue;
+        int rd = (int)p.a_rdiv;
+        asm volatile("" : "+v"(rd));  // keep the scatter address math here (not hoisted to kernel entry)
+        const int b = m / rd, pos = (int)p.a_roff + (m - b * rd);
+        bf16* base = j == 0 ? p.q + ((int64_t)b * p.H * p.S + pos) * 32 : p.k + ((int64_t)b * p.H * p.Npad + pos) * 32;
+        const int64_t hstride = (int64_t)(j == 0 ? p.S : p.Npad) * 32;
+#pragma unroll
+        for (int f = 0; f < GE / 16; ++f) {
+          const int n = f * 16 + fg * 4;  // 4 consecutive features, one head (32 | n)
+          bf16x4 o;
+          o[0] = (bf16)acc[f][tt][0], o[1] = (bf16)acc[f][tt][1];
+          o[2] = (bf16)acc[f][tt][2], o[3] = (bf16)acc[f][tt][3];
+          *(bf16x4*)(base + (n >> 5) * hstride + (n & 31)) = o;
+        }
+      }
+    } else {
+      panel_mma<false>(Ws, af, fr, fg, acc);
+      // C: lane = feature n (tile f, col fr); rows of the tile = rows m0 + 16tt + 4fg + i
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int ma = (int)(m0 + tt * 16 + fg * 4);
+        if (ma >= p.M) continue;
+        int rd = (int)p.a_rdiv;
+        asm volatile("" : "+v"(rd));
+        const int b = ma / rd, pos = (int)p.a_roff + (ma - b * rd);
+        const bool whole = ma + 3 < p.M && (ma - b * rd) + 3 < rd && (pos & 3) == 0;
+#pragma unroll
+        for (int f = 0; f < GE / 16; ++f) {
+          const int n = f * 16 + fr;
+          if (whole) {
+            bf16x4 o;
+            o[0] = (bf16)acc[f][tt][0], o[1] = (bf16)acc[f][tt][1];
+            o[2] = (bf16)acc[f][tt][2], o[3] = (bf16)acc[f][tt][3];
+            *(bf16x4*)(p.vt + ((int64_t)(b * p.H + (n >> 5)) * 32 + (n & 31)) * p.Npad + pos) = o;
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {  // fully unrolled: a runtime index would put acc in scratch
+              const int m = ma + i;
+              if (m < p.M) {
+                const int bi = m / rd, pi = (int)p.a_roff + (m - bi * rd);
+                p.vt[((int64_t)(bi * p.H + (n >> 5)) * 32 + (n & 31)) * p.Npad + pi] = (bf16)acc[f][tt][i];
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void rowgemm_resln_kernel(const RgArgs p) {
+  __shared__ __attribute__((aligned(16))) bf16 Ws[GE * WST];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * GROWS + wave * 32;
+  stage_panel(p.W, 0, Ws, tid);
+  bf16x8 af[2][GE / 32];
+  load_rows<false>(p, m0, fr, fg, af);
+  __syncthreads();
+  f32x4 y[GE / 16][2];
+  panel_mma<true>(Ws, af, fr, fg, y);
+  // Y^T: lane = row, rows of tile f = features 16f + 4fg + i
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int64_t m = m0 + tt * 16 + fr;
+    const bool valid = m < p.M;
+    float* xr = p.X + (valid ? m : (int64_t)p.M - 1) * GE + fg * 4;
+    float s = 0.f;
+#pragma unroll
+    for (int f = 0; f < GE / 16; ++f) {
+      const f32x4 xv = *(const f32x4*)(xr + f * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        y[f][tt][i] += xv[i];
+        s += y[f][tt][i];
+      }
+    }
+    s = sum_rows4(s);
+    const float mean = s * (1.0f / GE);
+    float q = 0.f;
+#pragma unroll
+    for (int f = 0; f < GE / 16; ++f)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float dl = y[f][tt][i] - mean;
+        q += dl * dl;
+      }
+    q = sum_rows4(q);
+    const float inv = 1.0f / sqrtf(q * (1.0f / GE) + p.eps);
+    if (valid) {
+#pragma unroll
+      for (int f = 0; f < GE / 16; ++f) {
+        f32x4 ov;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ov[i] = (y[f][tt][i] - mean) * inv;
+        *(f32x4*)(xr + f * 16) = ov;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
+                              const void* W, int M, int N, void* q, void* k, void* vt, int S, int Npad, int H,
+                              hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if ((N != GE && N != 3 * GE) || H * 32 != GE) return hipErrorInvalidValue;
+  RgArgs a{};
+  a.A = X, a.a_rdiv = a_rdiv, a.a_rmul = a_rmul, a.a_rmul2 = a_rmul2, a.a_roff = a_roff;
+  a.W = (const bf16*)W, a.M = M, a.N = N;
+  a.q = (bf16*)q, a.k = (bf16*)k, a.vt = (bf16*)vt, a.S = S, a.Npad = Npad, a.H = H;
+  const int npanels = N / GE;
+  hipLaunchKernelGGL(rowgemm_qkv_kernel, dim3(npanels * ((M + GROWS - 1) / GROWS)), dim3(256), 0, st, a, npanels);
+  return hipGetLastError();
+}
+
+hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, float* X, float eps, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  RgArgs a{};
+  a.A = O, a.a_rdiv = 1, a.a_rmul = 1, a.a_rmul2 = 0, a.a_roff = 0;
+  a.W = (const bf16*)W, a.M = (int)M, a.N = GE, a.X = X, a.eps = eps;
+  hipLaunchKernelGGL(rowgemm_resln_kernel, dim3((unsigned)((M + GROWS - 1) / GROWS)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace mmpfn
