@@ -85,7 +85,10 @@ def build_workload(device, world, members_per_gpu):
 
 
 def time_item_attention(eng, T, reps):
-    """Average launch duration of the sample-axis attention kernel at the workload's shape."""
+    """Average launch duration of the sample-axis attention kernel at the workload's shape.
+
+    One launch = the whole attention-between-items of one layer (train rows on their own
+    heads + test rows of all heads on head 0's K/V), HIP events on the engine stream."""
     from multimodalpfn_amd import _lib
 
     H, d, S, N = 6, 32, S_ROWS, N_TRAIN
@@ -101,27 +104,22 @@ def time_item_attention(eng, T, reps):
     eng._bind_stream()
     stream = torch.cuda.current_stream(dev)
 
-    def launch(s0, nq, kvh):
-        rc = lib.mmpfn_item_attention(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), S, T, H, Npad,
-                                      s0, nq, N, kvh, _lib.PREC_BF16)
+    def launch():
+        rc = lib.mmpfn_item_attention_layer(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), S, T, H,
+                                            Npad, N)
         assert rc == 0, lib.mmpfn_last_error(ctx)
 
-    res = {}
-    for name, (s0, nq, kvh, nqk) in {"train": (0, N, -1, N), "test": (N, Q, 0, Q)}.items():
-        for _ in range(3):
-            launch(s0, nq, kvh)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            launch(s0, nq, kvh)
-        e1.record(stream)
-        e1.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        flops = 4.0 * T * nqk * N * H * d
-        res[name] = (ms, flops)
-    ms_avg = (res["train"][0] + res["test"][0]) / 2
-    fl_avg = (res["train"][1] + res["test"][1]) / 2
-    achieved = fl_avg / (ms_avg * 1e-3) / 1e12
+    for _ in range(3):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        launch()
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flops = 4.0 * T * (N + Q) * N * H * d  # train 4*T*N*N*E + test (MQA) 4*T*Q*N*E
+    achieved = flops / (ms * 1e-3) / 1e12
     return {
         "bound": "mfma",
         "achieved": round(achieved, 1),
@@ -129,9 +127,9 @@ def time_item_attention(eng, T, reps):
         "unit": "TFLOP/s",
         "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
         "traffic": None,
-        "kernel": "attn_item_kernel<bf16> (sample-axis attention)",
-        "per_launch_ms": {"train_rows": round(res["train"][0], 4), "test_rows_mqa": round(res["test"][0], 4)},
-        "per_launch_flop": {"train_rows": res["train"][1], "test_rows_mqa": res["test"][1]},
+        "kernel": "attn_item2_kernel (sample-axis attention, train + test-MQA rows of one layer per launch)",
+        "per_launch_ms": round(ms, 4),
+        "per_launch_flop": flops,
     }
 
 

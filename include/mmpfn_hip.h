@@ -22,6 +22,9 @@
  *          transformer_encoder :799-808, decoder :850-853) for parity taps
  *   mmpfn_item_attention
  *       <- model/layer.py:341-379 attn_between_items (one token column batch)
+ *   mmpfn_item_attention_layer
+ *       <- model/layer.py:341-379 attn_between_items of one layer: train rows
+ *          (:362-372) and test rows against head 0's K/V (:344-358) together
  *   mmpfn_status
  *       <- model/transformer.py:727-731,790-796 NaN checks (ValueError)
  */
@@ -123,6 +126,12 @@ int mmpfn_status(mmpfn_ctx* ctx);
  * Element type: fp32 (MMPFN_PREC_F32) or bf16 (MMPFN_PREC_BF16). */
 int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S, int T,
                          int H, int Npad, int s0, int nq, int nk, int kv_head_fixed, int precision);
+
+/* The whole sample-axis attention of one layer in one launch (bf16 only): train queries
+ * s in [0, N) of head h against K/V head h, test queries s in [N, S) of every head against
+ * K/V head 0; keys [0, N).  Layouts as mmpfn_item_attention. */
+int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
+                               int T, int H, int Npad, int N);
 
 #ifdef __cplusplus
 }

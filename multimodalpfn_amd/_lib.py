@@ -68,6 +68,7 @@ SIGNATURES = [
     ("mmpfn_status", _i, [_vp]),
     ("mmpfn_aggregate", _i, [_vp, _vp, _i, _i, _i, _vp, _i, _f, _i, _vp, _vp]),
     ("mmpfn_item_attention", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i]),
+    ("mmpfn_item_attention_layer", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i]),
 ]
 
 _LIB = None

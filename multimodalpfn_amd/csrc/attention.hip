@@ -335,7 +335,317 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
   }
 }
 
+// ------------------------------------------------------------------ item attention v2 (bf16)
+// Sample-axis attention of one layer in ONE launch: the train rows against their own
+// head's K/V (layer.py:362-372) and the test rows of all heads against head 0's K/V
+// (multiquery_item_attention_for_test_set, layer.py:344-358) share the grid.  Work is
+// grouped by KV sequence (column b, kv head g): the queries that read (b, g) are
+//    own-head rows [a0, a0+na) of head g, then, for g == kvb, rows [b0, b0+nb) of all H heads,
+// cut into tasks of 256 queries = 4 waves x 64.  A block stages each 64-key K / V^T tile
+// once into LDS for its 4 waves; each wave runs two 32-query MFMA chains against it.
+//
+// Per 64-key tile and wave: 8 x v_mfma_f32_32x32x16_bf16 for S^T = K Q^T (query on the
+// lane), 8 for O^T += V^T P^T, 8 x v_mfma_f32_16x16x32_bf16 that sum P^T rows through a
+// 0/1 selector operand (the row sum never touches the VALU), 64 v_exp_f32 + 32 cvt_pk per
+// lane.  The softmax reference is FIXED after the first tile: m = that tile's row max, the
+// S^T chains start from the accumulator -m, p = exp2(s - m) feeds the MFMA unchanged.  No
+// per-tile max, no rescale.  Scaling by a power of two is exact, so the result equals the
+// running-max form up to rounding as long as no p overflows; p <= 2^100 is checked once at
+// the end (the row sum bounds every p) and a wave that fails it recomputes its queries with
+// an exact two-pass softmax (a1_exact_rows) -- a numerical backstop for score jumps of more
+// than ~88 (natural-log units) past the first tile's max, never taken on model data.
+//
+// LDS images (no padding, XOR-swizzled 16-B chunks; conflict-free ds_read_b128 for the
+// four 16-lane groups of a wave, MI355X_MICROARCH.md LDS table):
+//   K   [64 keys][32 d]  64-B rows : chunk c of row k at k*64 + 16*(c ^ ((k >> 2) & 3))
+//   V^T [32 d][64 keys] 128-B rows : chunk c of row d at d*128 + 16*(c ^ ((d >> 1) & 7)), keys
+//        inside every 16-key group stored in the order 0-3, 8-11, 4-7, 12-15 so that the
+//        keys one lane owns in the S^T accumulator (4hh + {0-3, 8-11}) are one 16-B chunk.
+constexpr int A2_KT = 64;
+constexpr int A2_NW = 4;
+constexpr int A2_QPB = A2_NW * 64;
+
+struct Attn2Args {
+  const bf16* q;  // [B][H][S][32]
+  const bf16* k;  // [B][H][Npad][32]
+  const bf16* vt; // [B][H][32][Npad]
+  bf16* o;        // row b*S + s, element row*H*32 + h*32 + d
+  int S, H, Npad, nk;
+  int a0, na;          // own-head query rows
+  int b0, nb, kvb;     // shared-KV query rows (all heads) against kv head kvb
+  int tasks_per_b, nblocks;
+  int tstart[9];       // task prefix per kv head inside one column
+};
+
+__device__ __forceinline__ int a2_koff(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
+__device__ __forceinline__ int a2_voff(int d, int c) { return d * 128 + 16 * (c ^ ((d >> 1) & 7)); }
+
+// exact two-pass softmax for one query per lane, K / V^T straight from global memory
+__device__ __attribute__((noinline)) void a1_exact_rows(const Attn2Args& p, const bf16* Kg, const bf16* Vg,
+                                                         const bf16* qrow, bf16* orow, bool valid) {
+  float q[32], o[32];
+  const float c = kLog2e * 0.17677669529663687f;
+#pragma unroll
+  for (int d = 0; d < 32; ++d) q[d] = (float)qrow[d] * c, o[d] = 0.f;
+  float m = -INFINITY;
+  for (int k = 0; k < p.nk; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) s = fmaf(q[d], (float)Kg[(int64_t)k * 32 + d], s);
+    m = fmaxf(m, s);
+  }
+  float l = 0.f;
+  for (int k = 0; k < p.nk; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) s = fmaf(q[d], (float)Kg[(int64_t)k * 32 + d], s);
+    const float e = exp2f(s - m);
+    l += e;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) o[d] = fmaf(e, (float)Vg[(int64_t)d * p.Npad + k], o[d]);
+  }
+  if (valid) {
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) orow[d] = (bf16)(o[d] * inv);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void attn_item2_kernel(const Attn2Args p) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2][2 * 4096];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+
+  // ---- task: contiguous task ranges per XCD (blocks of one KV sequence share an L2)
+  int b, g, chunk;
+  {
+    const int nbk = p.nblocks, pid = blockIdx.x;
+    const int xcd = pid & 7, slot = pid >> 3;
+    const int task = xcd * (nbk >> 3) + min(xcd, nbk & 7) + slot;
+    b = task / p.tasks_per_b;
+    const int rem = task - b * p.tasks_per_b;
+    g = 0;
+    while (g + 1 < p.H && p.tstart[g + 1] <= rem) ++g;
+    chunk = rem - p.tstart[g];
+  }
+  const int cnt = p.na + (g == p.kvb ? p.H * p.nb : 0);
+  const int jw = chunk * A2_QPB + wave * 64;  // first query of this wave
+  const bool active = jw < cnt;               // wave-uniform
+
+  const int64_t kvoff = ((int64_t)b * p.H + g) * p.Npad * 32;
+  const bf16* Kg = p.k + kvoff;
+  const bf16* Vg = p.vt + kvoff;
+  const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
+
+  // ---- the lane's query of each 32-query chain
+  int qh[2], qsrow[2];
+  bool qok[2];
+  bf16x8 qf[2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int j = jw + 32 * qb + r;
+    qok[qb] = j < cnt;
+    const int jc = min(j, cnt - 1);
+    if (jc < p.na) {
+      qh[qb] = g, qsrow[qb] = p.a0 + jc;
+    } else {
+      const int jj = jc - p.na;
+      qh[qb] = jj / p.nb, qsrow[qb] = p.b0 + jj % p.nb;
+    }
+    const bf16* qrow = p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 raw = *(const bf16x8*)(qrow + 16 * ks + 8 * hh);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (bf16)((float)raw[e] * c);
+    }
+  }
+
+  // ---- staging: one 16-B K chunk and one 16-B V^T chunk per thread and tile
+  const int krow = tid >> 2, kc = tid & 3;      // K tile [64][32]: row, chunk
+  const int vd = tid >> 3, vc = tid & 7;        // V^T tile [32][64]: row d, natural 8-key chunk
+  u32x4 rk, rv;
+  auto gload = [&](int k0, bool mask) {
+    rk = *(const u32x4*)(Kg + (int64_t)(k0 + krow) * 32 + kc * 8);
+    rv = *(const u32x4*)(Vg + (int64_t)vd * p.Npad + k0 + vc * 8);
+    if (mask) {  // keys >= nk: V = 0 so that p = 0 never meets NaN / inf padding
+      bf16x8 e = __builtin_bit_cast(bf16x8, rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (k0 + vc * 8 + j >= p.nk) e[j] = (bf16)0.0f;
+      rv = __builtin_bit_cast(u32x4, e);
+    }
+  };
+  const int koff_w = a2_koff(krow, kc);
+  const int voff_w0 = a2_voff(vd, vc & ~1) + 8 * (vc & 1), voff_w1 = a2_voff(vd, vc | 1) + 8 * (vc & 1);
+  auto lstore = [&](int buf) {
+    unsigned char* Ks = lds[buf];
+    *(u32x4*)(Ks + koff_w) = rk;
+    *(u32x2*)(Ks + 4096 + voff_w0) = u32x2{rv.x, rv.y};
+    *(u32x2*)(Ks + 4096 + voff_w1) = u32x2{rv.z, rv.w};
+  };
+  // fragment read offsets (bytes inside a stage)
+  int kro[2][2], vro[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      kro[u][i] = a2_koff(32 * u + r, 2 * i + hh);
+      vro[u][i] = 4096 + a2_voff(r, 2 * (2 * u + i) + hh);
+    }
+
+  // row-sum selector (A of v_mfma_f32_16x16x32_bf16): D row 0 sums k-groups 0 and 2 (queries
+  // 0-15 of the chain), row 1 sums k-groups 1 and 3 (queries 16-31); other rows zero.
+  bf16x8 sel;
+  {
+    const int m = lane & 15, kg = lane >> 4;
+    const bool one = (m == 0 && (kg & 1) == 0) || (m == 1 && (kg & 1) == 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sel[j] = (bf16)(one ? 1.0f : 0.0f);
+  }
+
+  f32x16 o[2], negm[2];
+  f32x4 lacc[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[qb][i] = negm[qb][i] = 0.f;
+    lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int ntiles = (p.nk + A2_KT - 1) / A2_KT;
+  const bool partial = (p.nk % A2_KT) != 0;
+
+  auto tile = [&](int it, auto maskc, auto firstc) {
+    constexpr bool MASK = decltype(maskc)::value;
+    constexpr bool FIRST = decltype(firstc)::value;
+    const int k0 = it * A2_KT;
+    if (it + 1 < ntiles) gload(k0 + A2_KT, partial && it + 2 == ntiles);
+    const unsigned char* Ks = lds[it & 1];
+    if (active) {
+      bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          kf[u][i] = *(const bf16x8*)(Ks + kro[u][i]);
+          vf[u][i] = *(const bf16x8*)(Ks + vro[u][i]);
+        }
+      f32x16 s[2][2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qf[qb][0], negm[qb], 0, 0, 0);
+          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][1], qf[qb][1], s[qb][u], 0, 0, 0);
+        }
+      if constexpr (MASK) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (k0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * hh >= p.nk) s[qb][u][i] = -INFINITY;
+      }
+      if constexpr (FIRST) {  // fix the reference max per query: this tile's row max
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          float m = fmaxf(s[qb][0][0], s[qb][1][0]);
+#pragma unroll
+          for (int i = 1; i < 16; ++i) m = fmaxf(m, fmaxf(s[qb][0][i], s[qb][1][i]));
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+          m = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            negm[qb][i] = -m;
+            s[qb][0][i] -= m;
+            s[qb][1][i] -= m;
+          }
+        }
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp) {
+            bf16x8 pb;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pb[j] = (bf16)__builtin_amdgcn_exp2f(s[qb][u][8 * sp + j]);
+            o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[u][sp], pb, o[qb], 0, 0, 0);
+            lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[qb], 0, 0, 0);
+          }
+    }
+    if (it + 1 < ntiles) lstore((it + 1) & 1);
+    __syncthreads();
+  };
+
+  gload(0, ntiles == 1 && partial);
+  lstore(0);
+  __syncthreads();
+  if (ntiles == 1) {
+    if (partial) tile(0, std::true_type{}, std::true_type{});
+    else tile(0, std::false_type{}, std::true_type{});
+  } else {
+    tile(0, std::false_type{}, std::true_type{});
+    const int nfull = p.nk / A2_KT;
+    for (int it = 1; it < nfull; ++it) tile(it, std::false_type{}, std::false_type{});
+    if (partial) tile(nfull, std::true_type{}, std::false_type{});
+  }
+  if (!active) return;
+
+  // ---- row sums to the query's lanes, overflow backstop, normalise, store
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const float a = __shfl(lacc[qb][0], lane & 15, 64), bsum = __shfl(lacc[qb][1], lane & 15, 64);
+    const float ls = r < 16 ? a : bsum;
+    bf16* orow = p.o + ((int64_t)b * p.S + qsrow[qb]) * (p.H * 32) + qh[qb] * 32;
+    // some p overflowed the fixed reference (sum >= 2^100, inf or NaN -- tested on the bits:
+    // this file builds with -fno-honor-nans): exact recompute
+    if (__any((__float_as_uint(ls) & 0x7fffffffu) >= 0x71800000u)) {
+      const bf16* qrow = p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
+      // lanes 0-31 own the chain's 32 queries; lanes 32-63 duplicate them and do not store
+      a1_exact_rows(p, Kg, Vg, qrow, orow, qok[qb] && hh == 0);
+      continue;
+    }
+    const float inv = 1.0f / ls;
+    if (qok[qb]) {
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        bf16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = (bf16)(o[qb][4 * gq + e] * inv);
+        *(bf16x4*)(orow + 8 * gq + 4 * hh) = w;
+      }
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
+                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st) {
+  if (na + nb <= 0 || T <= 0) return hipSuccess;
+  if (nk <= 0 || Npad % A2_KT != 0 || nk > Npad || H > 8 || H <= 0) return hipErrorInvalidValue;
+  if (nb > 0 && (kvb < 0 || kvb >= H)) return hipErrorInvalidValue;
+  Attn2Args a;
+  a.q = (const bf16*)q, a.k = (const bf16*)k, a.vt = (const bf16*)vt, a.o = (bf16*)out;
+  a.S = S, a.H = H, a.Npad = Npad, a.nk = nk;
+  a.a0 = a0, a.na = na, a.b0 = b0, a.nb = nb, a.kvb = nb > 0 ? kvb : -1;
+  int acc = 0;
+  for (int g = 0; g < H; ++g) {
+    a.tstart[g] = acc;
+    const int cnt = na + (g == a.kvb ? H * nb : 0);
+    acc += (cnt + A2_QPB - 1) / A2_QPB;
+  }
+  for (int g = H; g < 9; ++g) a.tstart[g] = acc;
+  a.tasks_per_b = acc;
+  a.nblocks = acc * T;
+  if (a.nblocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(attn_item2_kernel, dim3(a.nblocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int nw, hipStream_t st) {
   if (a.nq <= 0 || batches <= 0) return hipSuccess;
@@ -360,6 +670,10 @@ hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* 
   a.kv_bstride = (int64_t)H * Npad * 32, a.kv_hstride = (int64_t)Npad * 32, a.kpad = Npad;
   a.o_bstride = S, a.o_qstride = 1;
   a.s0 = s0, a.nq = nq, a.nk = nk, a.kvh_fixed = kv_head_fixed, a.H = H;
+  if (prec == PREC_BF16) {
+    if (kv_head_fixed < 0) return launch_attn_item2(q, k, vt, out, S, T, H, Npad, nk, s0, nq, 0, 0, -1, st);
+    return launch_attn_item2(q, k, vt, out, S, T, H, Npad, nk, 0, 0, s0, nq, kv_head_fixed, st);
+  }
   return launch_attn(a, T, prec, 4, st);
 }
 

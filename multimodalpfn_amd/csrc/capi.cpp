@@ -468,8 +468,12 @@ int run_layer(mmpfn_ctx* ctx, int l) {
         HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
       }
     }
-    HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, T, H, Npad, 0, N, N, -1, prec, st));
-    if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, T, H, Npad, N, Q, N, 0, prec, st));
+    if (bf) {  // train rows (own heads) and test rows (head-0 K/V, MQA) in one launch
+      HIPCHK(launch_attn_item2(Qi, Ki, Vi, O, S, T, H, Npad, N, 0, N, N, Q, 0, st));
+    } else {
+      HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, T, H, Npad, 0, N, N, -1, prec, st));
+      if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, T, H, Npad, N, Q, N, 0, prec, st));
+    }
     if (bf && E == 192) {
       HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, R, X, d.ln_eps, st));
     } else {
@@ -773,6 +777,16 @@ int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const voi
     return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(launch_attn_item(q, k, vt, out, S, T, H, Npad, s0, nq, nk, kvh, precision, ctx->stream));
+  return MMPFN_OK;
+}
+
+int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S, int T,
+                               int H, int Npad, int N) {
+  if (!ctx || !q || !k || !vt || !out) return MMPFN_ERR_INVALID;
+  if (N <= 0 || N > S || N > Npad || Npad % 64 || H <= 0 || H > 8 || T <= 0)
+    return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(launch_attn_item2(q, k, vt, out, S, T, H, Npad, N, 0, N, N, S - N, 0, ctx->stream));
   return MMPFN_OK;
 }
 

@@ -90,6 +90,11 @@ struct AttnArgs {
   int s0, nq, nk, kvh_fixed, H;
 };
 hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int waves_per_block, hipStream_t st);
+// bf16 sample-axis attention of one layer in one launch (attention.hip, attn_item2_kernel):
+//   own-head rows [a0, a0+na) of every head against that head's K/V, and rows [b0, b0+nb) of
+//   every head against K/V head kvb (nb = 0: none); keys [0, nk), Npad % 64 == 0
+hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
+                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st);
 // item attention: queries s in [s0, s0+nq), keys [0, nk); kv_head_fixed >= 0 forces that KV head
 hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
                             int Npad, int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st);

@@ -165,6 +165,67 @@ def test_item_attention_kernel(prec, S, N, T):
     assert (got.double() - ref).abs().max().item() < tol
 
 
+def _qkv_case(S, N, T, H=6, d=32, seed=0):
+    Npad = (N + 63) // 64 * 64
+    g = torch.Generator().manual_seed(seed)
+    q = torch.randn(T, H, S, d, generator=g)
+    k = torch.randn(T, H, N, d, generator=g)
+    v = torch.randn(T, H, N, d, generator=g)
+    return q, k, v, Npad
+
+
+def _launch_layer(q, k, v, Npad, N):
+    from multimodalpfn_amd import _lib
+    from multimodalpfn_amd.engine import HipEngine  # noqa: F401
+
+    T, H, S, d = q.shape
+    kp = torch.full((T, H, Npad, d), float("nan"))
+    kp[:, :, :N] = k
+    vt = torch.full((T, H, d, Npad), float("nan"))  # NaN padding must never leak
+    vt[:, :, :, :N] = v.transpose(-1, -2)
+    lib = _lib.load_library()
+    ctx = lib.mmpfn_create(0, None)
+    qd, kd, vd = q.to("cuda", torch.bfloat16), kp.to("cuda", torch.bfloat16), vt.to("cuda", torch.bfloat16)
+    out = torch.zeros(T, S, H * d, device="cuda", dtype=torch.bfloat16)
+    assert lib.mmpfn_item_attention_layer(ctx, qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), S, T, H,
+                                          Npad, N) == 0
+    torch.cuda.synchronize()
+    lib.mmpfn_destroy(ctx)
+    return out.float().cpu()
+
+
+def _layer_ref(q, k, v, N):
+    T, H, S, d = q.shape
+    qr, kr, vr = (t.to(torch.bfloat16).float() for t in (q, k, v))
+    ref_tr = _attn_ref(qr[:, :, :N], kr, vr)
+    ref_te = _attn_ref(qr[:, :, N:], kr[:, :1].expand_as(kr), vr[:, :1].expand_as(vr))
+    return torch.cat([ref_tr, ref_te], 2).permute(0, 2, 1, 3).reshape(T, S, H * d)
+
+
+@pytest.mark.parametrize("S,N,T", [(2298, 1838, 2), (70, 1, 2), (130, 64, 1), (200, 65, 3), (700, 333, 1)])
+def test_item_attention_layer_fused(S, N, T):
+    """One launch: train rows on their own heads + test rows of all heads on head 0 (MQA)."""
+    q, k, v, Npad = _qkv_case(S, N, T, seed=S + N)
+    got = _launch_layer(q, k, v, Npad, N)
+    ref = _layer_ref(q, k, v, N)
+    assert torch.isfinite(got).all()
+    assert (got.double() - ref).abs().max().item() < 2e-2
+
+
+def test_item_attention_overflow_backstop():
+    """Scores that jump far past the first key tile's max (p would overflow the fixed
+    softmax reference) take the exact two-pass recompute and still match."""
+    S, N, T = 300, 260, 1
+    q, k, v, Npad = _qkv_case(S, N, T, seed=5)
+    q[..., :] = q[..., :].sign() * 0.2 + 2.0  # all queries point along +1
+    k[:, :, 200:] = 6.0                       # late keys: scores ~ 2*6*32/sqrt(32) = 68 -> 2^98 over tile 0
+    k[:, :, 230:] = 9.0                       # ... and beyond the fp32 range of exp2(s - m_tile0)
+    got = _launch_layer(q, k, v, Npad, N)
+    ref = _layer_ref(q, k, v, N)
+    assert torch.isfinite(got).all()
+    assert (got.double() - ref).abs().max().item() < 2e-2
+
+
 def test_engine_deterministic_and_no_nan_at_pad_ufes_size():
     """Full config-C geometry (N=1838, Q=460, F=21, mgm 64 / cap 24): run twice, bitwise equal;
     bf16 vs fp32 engine argmax agreement (size-independent properties)."""
