@@ -127,6 +127,15 @@ int mmpfn_status(mmpfn_ctx* ctx);
 int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S, int T,
                          int H, int Npad, int s0, int nq, int nk, int kv_head_fixed, int precision);
 
+/* Forward lanes: independent per-member workspaces sharing the context's weights.
+ * Selects the lane used by the following embed / run_layers / decode / forward /
+ * copy_state calls (lane 0 at creation).  Members run concurrently when the caller binds a
+ * different stream (mmpfn_set_stream) to each lane; mmpfn_status checks every lane.
+ * Replaces nothing in the reference: its ensemble loop runs members one after another
+ * (inference.py:294-349); lanes let independent members overlap on one GPU. */
+#define MMPFN_MAX_LANES 8
+int mmpfn_select_lane(mmpfn_ctx* ctx, int lane);
+
 /* The whole sample-axis attention of one layer in one launch (bf16 only): train queries
  * s in [0, N) of head h against K/V head h, test queries s in [N, S) of every head against
  * K/V head 0; keys [0, N).  Layouts as mmpfn_item_attention. */

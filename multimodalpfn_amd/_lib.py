@@ -14,6 +14,7 @@ from pathlib import Path
 LIB_PATH = Path(__file__).resolve().parent / "libmmpfn_hip.so"
 
 MMPFN_OK = 0
+MMPFN_MAX_LANES = 8
 MMPFN_ERR_INVALID = -1
 MMPFN_ERR_HIP = -2
 MMPFN_ERR_NAN = -3
@@ -69,6 +70,7 @@ SIGNATURES = [
     ("mmpfn_aggregate", _i, [_vp, _vp, _i, _i, _i, _vp, _i, _f, _i, _vp, _vp]),
     ("mmpfn_item_attention", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i]),
     ("mmpfn_item_attention_layer", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i]),
+    ("mmpfn_select_lane", _i, [_vp, _i]),
 ]
 
 _LIB = None

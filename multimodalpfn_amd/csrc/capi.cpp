@@ -14,6 +14,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/mmpfn_hip.h"
@@ -60,12 +61,30 @@ struct mmpfn_ctx {
       cap_f3_b, cap_ng, cap_nb;
   DevBuf moe_w1, moe_w1_h, moe_b1, moe_w2, moe_w2_h, moe_b2, moe_gw, moe_gb;
 
-  // workspace
+  // workspace of the selected lane (per-member forward state)
   DevBuf ws_X, ws_O, ws_big, ws_pe, ws_slots, ws_scr, ws_flag;
   DevBuf mx[8];
   // current forward geometry
   int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0;
   bool embedded = false;
+  // lanes: independent forward workspaces sharing the weights, so members can run
+  // concurrently on different streams; the selected lane lives in the fields above and the
+  // others are parked here (mmpfn_select_lane swaps them)
+  struct Lane {
+    DevBuf ws_X, ws_O, ws_big, ws_pe, ws_slots, ws_scr, ws_flag;
+    int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0;
+    bool embedded = false;
+  };
+  std::vector<Lane> lanes;  // lanes[cur] is stale while cur is selected
+  int cur = 0;
+  template <typename A, typename B>
+  static void swap_lane(A& a, B& b) {
+    std::swap(a.ws_X, b.ws_X), std::swap(a.ws_O, b.ws_O), std::swap(a.ws_big, b.ws_big);
+    std::swap(a.ws_pe, b.ws_pe), std::swap(a.ws_slots, b.ws_slots), std::swap(a.ws_scr, b.ws_scr);
+    std::swap(a.ws_flag, b.ws_flag);
+    std::swap(a.S, b.S), std::swap(a.T, b.T), std::swap(a.N, b.N), std::swap(a.G, b.G), std::swap(a.C, b.C);
+    std::swap(a.Npad, b.Npad), std::swap(a.prec, b.prec), std::swap(a.embedded, b.embedded);
+  }
 };
 
 namespace {
@@ -639,7 +658,19 @@ void mmpfn_destroy(mmpfn_ctx* ctx) {
                     &ctx->ws_flag})
     fr(*b);
   for (auto& b : ctx->mx) fr(b);
+  for (auto& L : ctx->lanes)
+    for (DevBuf* b : {&L.ws_X, &L.ws_O, &L.ws_big, &L.ws_pe, &L.ws_slots, &L.ws_scr, &L.ws_flag}) fr(*b);
   delete ctx;
+}
+
+int mmpfn_select_lane(mmpfn_ctx* ctx, int lane) {
+  if (!ctx || lane < 0 || lane >= MMPFN_MAX_LANES) return MMPFN_ERR_INVALID;
+  if (lane == ctx->cur) return MMPFN_OK;
+  if ((int)ctx->lanes.size() < MMPFN_MAX_LANES) ctx->lanes.resize(MMPFN_MAX_LANES);
+  mmpfn_ctx::swap_lane(*ctx, ctx->lanes[ctx->cur]);   // park the selected lane
+  mmpfn_ctx::swap_lane(*ctx, ctx->lanes[lane]);       // bring the requested one in
+  ctx->cur = lane;
+  return MMPFN_OK;
 }
 
 const char* mmpfn_last_error(const mmpfn_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
@@ -762,9 +793,13 @@ int mmpfn_status(mmpfn_ctx* ctx) {
   if (!ctx) return MMPFN_ERR_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
-  if (ctx->ws_flag.p) {
+  std::vector<void*> flags{ctx->ws_flag.p};
+  for (size_t i = 0; i < ctx->lanes.size(); ++i)
+    if ((int)i != ctx->cur) flags.push_back(ctx->lanes[i].ws_flag.p);
+  for (void* fp : flags) {
+    if (!fp) continue;
     int f = 0;
-    HIPCHK(hipMemcpy(&f, ctx->ws_flag.p, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&f, fp, 4, hipMemcpyDeviceToHost));
     if (f) return fail(ctx, MMPFN_ERR_NAN, "There should be no NaNs in the encoded x and y (flag " + std::to_string(f) + ")");
   }
   return MMPFN_OK;

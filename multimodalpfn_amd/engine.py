@@ -13,6 +13,7 @@ shapes and the few host-side constants the reference also computes on the host:
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -60,6 +61,9 @@ def target_uniques(y_train: np.ndarray) -> np.ndarray:
     return np.unique(y).astype(np.float32)
 
 
+DEFAULT_LANES = int(os.environ.get("MMPFN_LANES", "2"))  # concurrent member lanes of forward_many
+
+
 class HipEngine:
     """One ``mmpfn_ctx`` bound to a CUDA(HIP) device."""
 
@@ -93,6 +97,8 @@ class HipEngine:
             raise _lib.EngineError(f"state_dict lacks {encoder_linear_name(cfg)}")
         self._check(self.lib.mmpfn_finalize_weights(self.ctx), "mmpfn_finalize_weights")
         self._pos_cache: dict[int, torch.Tensor] = {}
+        self._streams: list = []
+        self.lanes = DEFAULT_LANES
 
     # ------------------------------------------------------------------ plumbing
     def _stream(self) -> int:
@@ -179,6 +185,44 @@ class HipEngine:
         if check_nan:
             self.status()
         return out
+
+    def forward_many(self, items, precision: int, lanes: int | None = None) -> list[torch.Tensor]:
+        """Independent ensemble members ``[(x, tokens, y_train), ...]`` -> logits list.
+
+        Members are spread over ``lanes`` forward lanes (per-member workspaces of the same
+        context), each on its own HIP stream, so one member's kernels fill the tails and
+        latency gaps of another's.  The caller's stream waits for all of them.  The
+        reference runs its members one after another (inference.py:294-349); the results
+        do not depend on the lane count.
+        """
+        items = list(items)
+        if lanes is None:
+            lanes = self.lanes
+        lanes = max(1, min(int(lanes), len(items), _lib.MMPFN_MAX_LANES))
+        if lanes == 1:
+            return [self.forward(x, t, y, precision, check_nan=False) for x, t, y in items]
+        main = torch.cuda.current_stream(self.device)
+        streams = self._lane_streams(lanes)
+        for st in streams:
+            st.wait_stream(main)
+        outs = []
+        try:
+            for i, (x, t, y) in enumerate(items):
+                with torch.cuda.stream(streams[i % lanes]):
+                    self._check(self.lib.mmpfn_select_lane(self.ctx, i % lanes), "mmpfn_select_lane")
+                    outs.append(self.forward(x, t, y, precision, check_nan=False))
+        finally:
+            self._check(self.lib.mmpfn_select_lane(self.ctx, 0), "mmpfn_select_lane")
+            for st in streams:
+                main.wait_stream(st)
+        for o in outs:  # allocated on a lane stream, consumed on the caller's
+            o.record_stream(main)
+        return outs
+
+    def _lane_streams(self, n: int) -> list:
+        if len(self._streams) < n:
+            self._streams += [torch.cuda.Stream(self.device) for _ in range(n - len(self._streams))]
+        return self._streams[:n]
 
     def aggregate(self, logits: torch.Tensor, perms, n_classes: int, temperature: float,
                   average_before_softmax: bool, class_weights=None) -> torch.Tensor:

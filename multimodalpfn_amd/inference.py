@@ -71,7 +71,7 @@ class InferenceEngine:
         prec = _precision(model, eng.device, autocast, forced_dtype)
         mine, gather = member_shard(len(members), [self._member_cost(m, X, image_test) for m in members])
         tokens = _mixer_tokens(model, eng, image_train, image_test, prec) if mine else None
-        outs: dict[int, torch.Tensor] = {}
+        items = []
         for i in mine:
             m = members[i]
             if m.X_train is not None:
@@ -79,8 +79,9 @@ class InferenceEngine:
                 x_full = np.concatenate([np.asarray(m.X_train, np.float32), np.asarray(X_test, np.float32)], 0)
             else:
                 x_full = None
-            outs[i] = eng.forward(None if x_full is None else torch.from_numpy(x_full), tokens,
-                                  np.asarray(m.y_train, np.float32), prec, check_nan=False)
+            items.append((None if x_full is None else torch.from_numpy(x_full), tokens,
+                          np.asarray(m.y_train, np.float32)))
+        outs: dict[int, torch.Tensor] = dict(zip(mine, eng.forward_many(items, prec)))
         if mine:
             eng.status()  # NaN / HIP errors of every queued member (transformer.py:727-731,790-796)
         Q = len(X) if X is not None else len(image_test)

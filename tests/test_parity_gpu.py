@@ -248,3 +248,34 @@ def test_engine_deterministic_and_no_nan_at_pad_ufes_size():
     assert torch.equal(a, b)
     assert torch.isfinite(c).all()
     assert (a.argmax(-1) == c.argmax(-1)).float().mean() > 0.9
+
+
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_forward_lanes_match_sequential(lanes):
+    """Members on concurrent lanes (own workspace + stream each) == one after another, bitwise."""
+    from synth import synth_image, synth_labels, synth_state_dict, synth_table
+
+    from multimodalpfn_amd import _lib
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    cfg = ModelConfig(nlayers=3, mgm_heads=8, cap_heads=4)
+    sd = synth_state_dict(state_dict_spec(cfg), 4)
+    model = make_model(cfg, sd)
+    eng = model.engine()
+    S, N, F = 300, 230, 9
+    x = synth_table(S, F, 4, n_cat=3)
+    im = torch.from_numpy(synth_image(S, 1, 4)).cuda()
+    y = synth_labels(S, 3, 4)[:N]
+    tok = eng.mixer_tokens(im, _lib.PREC_BF16)
+    rng = np.random.default_rng(1)
+    items = []
+    for m in range(5):
+        xm = torch.from_numpy(np.ascontiguousarray(x[:, rng.permutation(F)]))
+        ym = rng.permutation(3)[y.astype(np.int64)].astype(np.float32)
+        items.append((xm, tok, ym))
+    with torch.inference_mode():
+        seq = eng.forward_many(items, _lib.PREC_BF16, lanes=1)
+        par = eng.forward_many(items, _lib.PREC_BF16, lanes=lanes)
+        eng.status()
+    for a, b in zip(seq, par):
+        assert torch.equal(a.cpu(), b.cpu())
