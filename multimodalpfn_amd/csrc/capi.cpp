@@ -32,6 +32,7 @@ struct DevBuf {
 struct LayerW {  // packed per layer, [N][K] row-major
   DevBuf feat_qkv, feat_out, item_qkv, item_qtest, item_out, mlp1, mlp2;  // fp32
   DevBuf feat_qkv_h, feat_out_h, item_qkv_h, item_qtest_h, item_out_h, mlp1_h, mlp2_h;  // bf16
+  DevBuf feat_pack_h;  // bf16, per head [permuted QKV slice | permuted Wout slice] (featrow.hip)
 };
 
 uint16_t f2bf(float f) {  // round-to-nearest-even, NaN preserving
@@ -166,6 +167,35 @@ std::vector<float> pack_mlp2_perm(const std::vector<float>& w, int E, int Fh) {
   return o;
 }
 
+// featrow.hip weight pack, per head h (FEAT_PACK_HEAD floats):
+//   rows [0,32)  : Wq row 8*(r>>2 & 3) + 4*(r>>4) + (r&3) for r = 16f + rho -> head dim 8(rho>>2)+4f+(rho&3),
+//                  scaled by log2(e)/sqrt(32) (the feature-attention softmax scale, exp2 domain)
+//   rows [32,64) : Wk, same row permutation;   rows [64,96): Wv in natural order
+//   then [192][32] : Wout[e][h*32 + perm(c)], perm(8g+j) = j<4 ? 4g+j : 16+4g+(j-4)
+// qkv: w_qkv [3][H][32][E] (multi_head_attention.py:423-430); wout_t: [E][H*32]
+std::vector<float> pack_feat_rows(const std::vector<float>& qkv, const std::vector<float>& wout_t, int H, int E) {
+  const float c = 1.4426950408889634f / std::sqrt(32.0f);
+  std::vector<float> o((size_t)H * FEAT_PACK_HEAD);
+  for (int h = 0; h < H; ++h) {
+    float* ph = o.data() + (size_t)h * FEAT_PACK_HEAD;
+    for (int r = 0; r < 96; ++r) {
+      const int j = r / 32, rr = r % 32, f = rr >> 4, rho = rr & 15;
+      const int dd = j < 2 ? 8 * (rho >> 2) + 4 * f + (rho & 3) : rr;
+      const float sc = j == 0 ? c : 1.0f;
+      const float* src = qkv.data() + ((size_t)(j * H + h) * 32 + dd) * E;
+      for (int k = 0; k < E; ++k) ph[(size_t)r * E + k] = src[k] * sc;
+    }
+    float* po = ph + 96 * E;
+    for (int e = 0; e < E; ++e)
+      for (int cc = 0; cc < 32; ++cc) {
+        const int g = cc >> 3, jj = cc & 7;
+        const int dd = jj < 4 ? 4 * g + jj : 16 + 4 * g + (jj - 4);
+        po[(size_t)e * 32 + cc] = wout_t[(size_t)e * H * 32 + h * 32 + dd];
+      }
+  }
+  return o;
+}
+
 int up2(mmpfn_ctx* ctx, DevBuf& f, DevBuf& h, const std::vector<float>& v) {
   int rc = upload(ctx, f, v, false);
   if (rc) return rc;
@@ -199,6 +229,9 @@ int finalize(mmpfn_ctx* ctx) {
     GETW(m2, p + "mlp.linear2.weight", (size_t)E * Fh);
     if ((rc = up2(ctx, L.feat_qkv, L.feat_qkv_h, *fq))) return rc;
     if ((rc = up2(ctx, L.feat_out, L.feat_out_h, transpose_out(*fo, HD, E)))) return rc;
+    if (E == 192 && d.nhead == 6)
+      if ((rc = upload(ctx, L.feat_pack_h, pack_feat_rows(*fq, transpose_out(*fo, HD, E), d.nhead, E), true)))
+        return rc;
     if ((rc = up2(ctx, L.item_out, L.item_out_h, transpose_out(*io, HD, E)))) return rc;
     if ((rc = up2(ctx, L.mlp1, L.mlp1_h, *m1))) return rc;
     if ((rc = upload(ctx, L.mlp2, *m2, false))) return rc;
@@ -436,7 +469,10 @@ int run_layer(mmpfn_ctx* ctx, int l) {
   unsigned char* big = (unsigned char*)ctx->ws_big.p;
 
   // ---- attention between features (layer.py:332-339): batch = row s, T tokens
-  if (bf && d.nhead * 32 == E && feat_block_rows(T) > 0) {
+  if (bf && L.feat_pack_h.p && T <= 64) {
+    // one wave per row, the whole sublayer in registers (featrow.hip)
+    HIPCHK(launch_feat_rows(X, L.feat_pack_h.p, S, T, E, H, d.ln_eps, st));
+  } else if (bf && d.nhead * 32 == E && feat_block_rows(T) > 0) {
     // one fused kernel: QKV, per-row attention, out-projection, residual + LN out of LDS
     HIPCHK(launch_feat_block(X, L.feat_qkv_h.p, L.feat_out_h.p, S, T, E, H, d.ln_eps, st));
   } else {
@@ -645,7 +681,7 @@ void mmpfn_destroy(mmpfn_ctx* ctx) {
   for (auto& L : ctx->layers) {
     for (DevBuf* b : {&L.feat_qkv, &L.feat_out, &L.item_qkv, &L.item_qtest, &L.item_out, &L.mlp1, &L.mlp2,
                       &L.feat_qkv_h, &L.feat_out_h, &L.item_qkv_h, &L.item_qtest_h, &L.item_out_h, &L.mlp1_h,
-                      &L.mlp2_h})
+                      &L.mlp2_h, &L.feat_pack_h})
       fr(*b);
   }
   for (DevBuf* b : {&ctx->enc_w, &ctx->y_w, &ctx->y_b, &ctx->pe_w, &ctx->pe_b, &ctx->dec_w1, &ctx->dec_b1,
