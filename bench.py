@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--attn-reps", type=int, default=20)
     p.add_argument("--lanes", type=int, default=None, help="concurrent member lanes per GPU (default: engine's)")
+    p.add_argument("--batch", type=int, default=None, help="members per batched forward (default: engine's)")
     p.add_argument("--api-steps", type=int, default=3, help="timed predict_proba calls of the API leg (0: skip)")
     return p.parse_args()
 
@@ -235,7 +236,8 @@ def main():
 
     def step():
         tokens = eng.mixer_tokens(img, prec)
-        outs = eng.forward_many([(members[m][0], tokens, members[m][1]) for m in mine], prec, args.lanes)
+        outs = eng.forward_many([(members[m][0], tokens, members[m][1]) for m in mine], prec, args.lanes,
+                                args.batch)
         local = torch.stack(outs)
         allm = allgather_logits(local, assignment, rank)
         return eng.aggregate(allm, perms, N_CLASSES, 0.9, False)
@@ -291,6 +293,7 @@ def main():
                             "(18 cat + 3 num), image [S,1,768], MGM 64 heads + CAP 24, 12 layers E=192",
                 "members_per_gpu": args.members,
                 "lanes": eng.lanes if args.lanes is None else args.lanes,
+                "members_per_batched_forward": eng.batch if args.batch is None else args.batch,
                 "members_total": M,
                 "rows_per_member": S_ROWS,
                 "tokens_per_row": T,

@@ -127,6 +127,16 @@ int mmpfn_status(mmpfn_ctx* ctx);
 int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S, int T,
                          int H, int Npad, int s0, int nq, int nk, int kv_head_fixed, int precision);
 
+/* M ensemble members of one geometry (same S, N, F, C) in one batched forward: the
+ * state of all members is stacked [M][T][S][E] so every layer kernel runs once over the
+ * batch (M*S rows, M*T attention columns).  x, y, uniq: HOST arrays of M device pointers
+ * (as mmpfn_forward's arguments of each member); U: host array of M unique-label counts;
+ * logits: device [M][S-N][n_out].  Replaces the per-member model call of the ensemble loop
+ * (inference.py:294-349 -> transformer.py:462-545) for members that share a geometry. */
+int mmpfn_forward_batch(mmpfn_ctx* ctx, int M, const float* const* x, int S, int F, const float* tokens, int C,
+                        const float* const* y, int N, const float* const* uniq, const int* U,
+                        const float* pos_rand, float* logits, int precision);
+
 /* Forward lanes: independent per-member workspaces sharing the context's weights.
  * Selects the lane used by the following embed / run_layers / decode / forward /
  * copy_state calls (lane 0 at creation).  Members run concurrently when the caller binds a

@@ -65,15 +65,15 @@ struct mmpfn_ctx {
   // workspace of the selected lane (per-member forward state)
   DevBuf ws_X, ws_O, ws_big, ws_pe, ws_slots, ws_scr, ws_flag;
   DevBuf mx[8];
-  // current forward geometry
-  int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0;
+  // current forward geometry (M members of equal geometry stacked as [M][T][S][E])
+  int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0, M = 1;
   bool embedded = false;
   // lanes: independent forward workspaces sharing the weights, so members can run
   // concurrently on different streams; the selected lane lives in the fields above and the
   // others are parked here (mmpfn_select_lane swaps them)
   struct Lane {
     DevBuf ws_X, ws_O, ws_big, ws_pe, ws_slots, ws_scr, ws_flag;
-    int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0;
+    int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0, M = 1;
     bool embedded = false;
   };
   std::vector<Lane> lanes;  // lanes[cur] is stale while cur is selected
@@ -84,7 +84,7 @@ struct mmpfn_ctx {
     std::swap(a.ws_pe, b.ws_pe), std::swap(a.ws_slots, b.ws_slots), std::swap(a.ws_scr, b.ws_scr);
     std::swap(a.ws_flag, b.ws_flag);
     std::swap(a.S, b.S), std::swap(a.T, b.T), std::swap(a.N, b.N), std::swap(a.G, b.G), std::swap(a.C, b.C);
-    std::swap(a.Npad, b.Npad), std::swap(a.prec, b.prec), std::swap(a.embedded, b.embedded);
+    std::swap(a.Npad, b.Npad), std::swap(a.prec, b.prec), std::swap(a.embedded, b.embedded), std::swap(a.M, b.M);
   }
 };
 
@@ -412,8 +412,9 @@ GemmArgs gargs() {
     if (rc_ != MMPFN_OK) return rc_; \
   } while (0)
 
+// member m (of M, all of the geometry set by member 0) -> X[m] = embedded input [T][S][E]
 int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int C, const float* y, int N,
-          const float* uniq, int U, const float* pos_rand, int prec) {
+          const float* uniq, int U, const float* pos_rand, int prec, int m = 0, int M = 1) {
   const mmpfn_model_desc& d = ctx->d;
   if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
   if (S <= 0 || N <= 0 || N > S || (x && F <= 0) || C < 0 || U <= 0)
@@ -424,23 +425,30 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
   const int G = x ? (F + fpg - 1) / fpg : 0;
   const int T = G + C + 1;
   const int Npad = (N + 63) / 64 * 64;
-  ctx->S = S, ctx->T = T, ctx->N = N, ctx->G = G, ctx->C = C, ctx->Npad = Npad, ctx->prec = prec;
   const size_t R = (size_t)S * T;
-  RC(ensure(ctx, ctx->ws_X, R * E * 4));
-  RC(ensure(ctx, ctx->ws_O, R * E * 4));
-  const size_t Tpad = (T + 63) / 64 * 64;
-  const size_t big = std::max(R * E + (size_t)2 * S * Tpad * E, R * E + (size_t)2 * T * Npad * E) * 4;
-  RC(ensure(ctx, ctx->ws_big, big));
-  RC(ensure(ctx, ctx->ws_pe, (size_t)(G + C + 1) * E * 4));
-  RC(ensure(ctx, ctx->ws_slots, (size_t)(G + 1) * fpg * sizeof(SlotParams)));
-  RC(ensure(ctx, ctx->ws_scr, 256));
-  RC(ensure(ctx, ctx->ws_flag, 256));
   hipStream_t st = ctx->stream;
-  float* X = (float*)ctx->ws_X.p;
-  int* flag = (int*)ctx->ws_flag.p;
-  HIPCHK(hipMemsetAsync(flag, 0, 4, st));
-  HIPCHK(launch_pos_emb(pos_rand, G + C, (const float*)ctx->pe_w.p, (const float*)ctx->pe_b.p, (float*)ctx->ws_pe.p, E,
-                        st));
+  int* flag;
+  if (m == 0) {
+    ctx->S = S, ctx->T = T, ctx->N = N, ctx->G = G, ctx->C = C, ctx->Npad = Npad, ctx->prec = prec, ctx->M = M;
+    RC(ensure(ctx, ctx->ws_X, (size_t)M * R * E * 4));
+    RC(ensure(ctx, ctx->ws_O, (size_t)M * R * E * 4));
+    const size_t Tpad = (T + 63) / 64 * 64;
+    const size_t big = std::max(R * E + (size_t)2 * S * Tpad * E, (size_t)M * (R * E + (size_t)2 * T * Npad * E)) * 4;
+    RC(ensure(ctx, ctx->ws_big, big));
+    RC(ensure(ctx, ctx->ws_pe, (size_t)(G + C + 1) * E * 4));
+    RC(ensure(ctx, ctx->ws_slots, (size_t)(G + 1) * fpg * sizeof(SlotParams)));
+    RC(ensure(ctx, ctx->ws_scr, 256));
+    RC(ensure(ctx, ctx->ws_flag, 256));
+    flag = (int*)ctx->ws_flag.p;
+    HIPCHK(hipMemsetAsync(flag, 0, 4, st));
+    HIPCHK(launch_pos_emb(pos_rand, G + C, (const float*)ctx->pe_w.p, (const float*)ctx->pe_b.p,
+                          (float*)ctx->ws_pe.p, E, st));
+  } else {
+    if (S != ctx->S || T != ctx->T || N != ctx->N || G != ctx->G || C != ctx->C || prec != ctx->prec || m >= ctx->M)
+      return fail(ctx, MMPFN_ERR_INVALID, "batched members must share S, N, F, C and precision");
+    flag = (int*)ctx->ws_flag.p;
+  }
+  float* X = (float*)ctx->ws_X.p + (size_t)m * R * E;
   if (G) {
     HIPCHK(launch_encode_x(x, S, F, N, G, fpg, d.encoder_features, d.outlier_sigma, (SlotParams*)ctx->ws_slots.p,
                            (const float*)ctx->enc_w.p, (const float*)ctx->ws_pe.p, X, E, flag, st));
@@ -458,98 +466,105 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
 int run_layer(mmpfn_ctx* ctx, int l) {
   const mmpfn_model_desc& d = ctx->d;
   const LayerW& L = ctx->layers[l];
-  const int S = ctx->S, T = ctx->T, N = ctx->N, Npad = ctx->Npad, prec = ctx->prec;
+  const int S = ctx->S, T = ctx->T, N = ctx->N, Npad = ctx->Npad, prec = ctx->prec, M = ctx->M;
   const int E = d.emsize, H = d.nhead, Q = S - N;
-  const int64_t R = (int64_t)S * T;
+  const int64_t R = (int64_t)S * T;  // tokens of one member
+  const int64_t RM = R * M;          // tokens of the batch
+  const int TM = T * M;              // token columns of the batch (attention batches)
   const bool bf = prec == PREC_BF16;
   const int eb = bf ? 2 : 4;
   hipStream_t st = ctx->stream;
-  float* X = (float*)ctx->ws_X.p;
+  float* Xall = (float*)ctx->ws_X.p;
   void* O = ctx->ws_O.p;
   unsigned char* big = (unsigned char*)ctx->ws_big.p;
 
   // ---- attention between features (layer.py:332-339): batch = row s, T tokens
   if (bf && L.feat_pack_h.p && T <= 64) {
-    // one wave per row, the whole sublayer in registers (featrow.hip)
-    HIPCHK(launch_feat_rows(X, L.feat_pack_h.p, S, T, E, H, d.ln_eps, st));
-  } else if (bf && d.nhead * 32 == E && feat_block_rows(T) > 0) {
-    // one fused kernel: QKV, per-row attention, out-projection, residual + LN out of LDS
-    HIPCHK(launch_feat_block(X, L.feat_qkv_h.p, L.feat_out_h.p, S, T, E, H, d.ln_eps, st));
+    // one wave per row (all M members' rows in one launch), the whole sublayer in registers (featrow.hip)
+    HIPCHK(launch_feat_rows(Xall, L.feat_pack_h.p, S, T, M, E, H, d.ln_eps, st));
   } else {
-    const int Tpad = (T + 63) / 64 * 64;
-    void* Qf = big;
-    void* Kf = big + (size_t)R * E * eb;
-    void* Vf = (unsigned char*)Kf + (size_t)S * H * Tpad * 32 * eb;
-    GemmArgs a = gargs();
-    // logical rows m = s*T + t: A row t*S + s; scatter batch b = s, position t
-    a.A = X, a.lda = E, a.a_rdiv = T, a.a_rmul = 1, a.a_rmul2 = S;
-    a.W = W(L.feat_qkv, L.feat_qkv_h, prec);
-    a.M = (int)R, a.N = 3 * E, a.K = E;
-    a.q = Qf, a.k = Kf, a.v = Vf, a.S = T, a.Npad = Tpad, a.T = T, a.H = H;
-    HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
-    AttnArgs f;
-    f.q = Qf, f.k = Kf, f.vt = Vf, f.o = O;
-    f.q_bstride = (int64_t)H * T * 32, f.q_hstride = (int64_t)T * 32;
-    f.kv_bstride = (int64_t)H * Tpad * 32, f.kv_hstride = (int64_t)Tpad * 32, f.kpad = Tpad;
-    f.o_bstride = 1, f.o_qstride = S;  // O[t][s]
-    f.s0 = 0, f.nq = T, f.nk = T, f.kvh_fixed = -1, f.H = H;
-    HIPCHK(launch_attn(f, S, prec, 1, st));
-    GemmArgs b = gargs();
-    b.A = O, b.lda = E, b.W = W(L.feat_out, L.feat_out_h, prec);
-    b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
-    HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
+    for (int m = 0; m < M; ++m) {  // member by member (the scratch holds one member)
+      float* X = Xall + (size_t)m * R * E;
+      if (bf && d.nhead * 32 == E && feat_block_rows(T) > 0) {
+        HIPCHK(launch_feat_block(X, L.feat_qkv_h.p, L.feat_out_h.p, S, T, E, H, d.ln_eps, st));
+        continue;
+      }
+      const int Tpad = (T + 63) / 64 * 64;
+      void* Qf = big;
+      void* Kf = big + (size_t)R * E * eb;
+      void* Vf = (unsigned char*)Kf + (size_t)S * H * Tpad * 32 * eb;
+      GemmArgs a = gargs();
+      // logical rows m = s*T + t: A row t*S + s; scatter batch b = s, position t
+      a.A = X, a.lda = E, a.a_rdiv = T, a.a_rmul = 1, a.a_rmul2 = S;
+      a.W = W(L.feat_qkv, L.feat_qkv_h, prec);
+      a.M = (int)R, a.N = 3 * E, a.K = E;
+      a.q = Qf, a.k = Kf, a.v = Vf, a.S = T, a.Npad = Tpad, a.T = T, a.H = H;
+      HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+      AttnArgs f;
+      f.q = Qf, f.k = Kf, f.vt = Vf, f.o = O;
+      f.q_bstride = (int64_t)H * T * 32, f.q_hstride = (int64_t)T * 32;
+      f.kv_bstride = (int64_t)H * Tpad * 32, f.kv_hstride = (int64_t)Tpad * 32, f.kpad = Tpad;
+      f.o_bstride = 1, f.o_qstride = S;  // O[t][s]
+      f.s0 = 0, f.nq = T, f.nk = T, f.kvh_fixed = -1, f.H = H;
+      HIPCHK(launch_attn(f, S, prec, 1, st));
+      GemmArgs b = gargs();
+      b.A = O, b.lda = E, b.W = W(L.feat_out, L.feat_out_h, prec);
+      b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
+      HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
+    }
   }
-  // ---- attention between items (layer.py:341-379)
+  // ---- attention between items (layer.py:341-379); rows of all members: logical row
+  //      (member*T + t)*N + n -> memory row (member*T + t)*S + n, attention batch member*T + t
   {
     void* Qi = big;
-    void* Ki = big + (size_t)R * E * eb;
-    void* Vi = (unsigned char*)Ki + (size_t)T * H * Npad * 32 * eb;
+    void* Ki = big + (size_t)RM * E * eb;
+    void* Vi = (unsigned char*)Ki + (size_t)TM * H * Npad * 32 * eb;
     if (bf && E == 192) {  // row-resident projections straight into the attention layouts
-      HIPCHK(launch_rowgemm_qkv(X, N, S, 1, 0, L.item_qkv_h.p, T * N, 3 * E, Qi, Ki, Vi, S, Npad, H, st));
+      HIPCHK(launch_rowgemm_qkv(Xall, N, S, 1, 0, L.item_qkv_h.p, TM * N, 3 * E, Qi, Ki, Vi, S, Npad, H, st));
       if (Q > 0)
-        HIPCHK(launch_rowgemm_qkv(X, Q, S, 1, N, L.item_qtest_h.p, T * Q, E, Qi, Ki, Vi, S, Npad, H, st));
+        HIPCHK(launch_rowgemm_qkv(Xall, Q, S, 1, N, L.item_qtest_h.p, TM * Q, E, Qi, Ki, Vi, S, Npad, H, st));
     } else {
       GemmArgs a = gargs();
-      a.A = X, a.lda = E, a.a_rdiv = N, a.a_rmul = S, a.a_roff = 0;
+      a.A = Xall, a.lda = E, a.a_rdiv = N, a.a_rmul = S, a.a_roff = 0;
       a.W = W(L.item_qkv, L.item_qkv_h, prec);
-      a.M = T * N, a.N = 3 * E, a.K = E;
-      a.q = Qi, a.k = Ki, a.v = Vi, a.S = S, a.Npad = Npad, a.T = T, a.H = H;
+      a.M = TM * N, a.N = 3 * E, a.K = E;
+      a.q = Qi, a.k = Ki, a.v = Vi, a.S = S, a.Npad = Npad, a.T = TM, a.H = H;
       HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
       if (Q > 0) {
         GemmArgs c = a;
         c.a_rdiv = Q, c.a_roff = N;
         c.W = W(L.item_qtest, L.item_qtest_h, prec);
-        c.M = T * Q, c.N = E;
+        c.M = TM * Q, c.N = E;
         HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
       }
     }
     if (bf) {  // train rows (own heads) and test rows (head-0 K/V, MQA) in one launch
-      HIPCHK(launch_attn_item2(Qi, Ki, Vi, O, S, T, H, Npad, N, 0, N, N, Q, 0, st));
+      HIPCHK(launch_attn_item2(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st));
     } else {
-      HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, T, H, Npad, 0, N, N, -1, prec, st));
-      if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, T, H, Npad, N, Q, N, 0, prec, st));
+      HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, 0, N, N, -1, prec, st));
+      if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, N, Q, N, 0, prec, st));
     }
     if (bf && E == 192) {
-      HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, R, X, d.ln_eps, st));
+      HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, RM, Xall, d.ln_eps, st));
     } else {
       GemmArgs b = gargs();
       b.A = O, b.lda = E, b.W = W(L.item_out, L.item_out_h, prec);
-      b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
+      b.M = (int)RM, b.N = E, b.K = E, b.X = Xall, b.ln_eps = d.ln_eps;
       HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
     }
   }
-  // ---- MLP (mlp.py:93-104), fused up/GELU/down/residual/LN
+  // ---- MLP (mlp.py:93-104), fused up/GELU/down/residual/LN, all members' tokens
   if (bf && d.nhid % 32 == 0)  // W2 bf16 copy is stored in mlp_rows_kernel's permuted K order
-    HIPCHK(launch_mlp_rows(X, L.mlp1_h.p, L.mlp2_h.p, R, E, d.nhid, d.ln_eps, st));
+    HIPCHK(launch_mlp_rows(Xall, L.mlp1_h.p, L.mlp2_h.p, RM, E, d.nhid, d.ln_eps, st));
   else
-    HIPCHK(launch_mlp_fused(X, L.mlp1.p, L.mlp2.p, R, E, d.nhid, d.ln_eps, PREC_F32, st));
+    HIPCHK(launch_mlp_fused(Xall, L.mlp1.p, L.mlp2.p, RM, E, d.nhid, d.ln_eps, PREC_F32, st));
   return MMPFN_OK;
 }
 
-int decode(mmpfn_ctx* ctx, float* logits) {
+int decode(mmpfn_ctx* ctx, float* logits, int m = 0) {
   const mmpfn_model_desc& d = ctx->d;
   const int E = d.emsize, S = ctx->S, T = ctx->T, N = ctx->N;
-  const float* Xl = (const float*)ctx->ws_X.p + ((size_t)(T - 1) * S + N) * E;
+  const float* Xl = (const float*)ctx->ws_X.p + (size_t)m * S * T * E + ((size_t)(T - 1) * S + N) * E;
   HIPCHK(launch_decoder(Xl, S - N, (const float*)ctx->dec_w1.p, (const float*)ctx->dec_b1.p, d.nhid,
                         (const float*)ctx->dec_w2.p, (const float*)ctx->dec_b2.p, d.n_out, logits, E, ctx->stream));
   return MMPFN_OK;
@@ -801,6 +816,20 @@ int mmpfn_forward(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tok
   RC(embed(ctx, x, S, F, tokens, C, y, N, uniq, U, pos_rand, precision));
   for (int l = 0; l < ctx->d.nlayers; ++l) RC(run_layer(ctx, l));
   return decode(ctx, logits);
+}
+
+int mmpfn_forward_batch(mmpfn_ctx* ctx, int M, const float* const* x, int S, int F, const float* tokens, int C,
+                        const float* const* y, int N, const float* const* uniq, const int* U, const float* pos_rand,
+                        float* logits, int precision) {
+  if (!ctx || !logits || M <= 0 || !y || !uniq || !U) return MMPFN_ERR_INVALID;
+  if (F > 0 && !x) return MMPFN_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  for (int m = 0; m < M; ++m)
+    RC(embed(ctx, F > 0 ? x[m] : nullptr, S, F, tokens, C, y[m], N, uniq[m], U[m], pos_rand, precision, m, M));
+  for (int l = 0; l < ctx->d.nlayers; ++l) RC(run_layer(ctx, l));
+  const size_t per = (size_t)(S - N) * ctx->d.n_out;
+  for (int m = 0; m < M; ++m) RC(decode(ctx, logits + m * per, m));
+  return MMPFN_OK;
 }
 
 int mmpfn_state_tokens(const mmpfn_ctx* ctx) { return ctx ? ctx->T : 0; }

@@ -49,15 +49,17 @@ __device__ __forceinline__ bf16x8 cat8(const f32x4& a, const f32x4& b, float s =
 }
 
 template <int NT>
-__global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ X, const bf16* __restrict__ pack,
-                                                           int S, int T, float eps) {
+__global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ Xall, const bf16* __restrict__ pack,
+                                                           int S, int T, int M, float eps) {
   __shared__ __attribute__((aligned(16))) bf16 wbuf[2 * FR_BUF_EL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
-  const int s = blockIdx.x * 4 + wave;
-  const bool rowok = s < S;  // wave-uniform; a wave past the last row computes row S-1 and stores nothing
-  const int sr = rowok ? s : S - 1;
+  const int row = blockIdx.x * 4 + wave;  // row over the batch: member row / S, table row row % S
+  const bool rowok = row < M * S;  // wave-uniform; a wave past the last row recomputes it and stores nothing
+  const int rc = rowok ? row : M * S - 1;
+  const int mem = rc / S, sr = rc - mem * S;
   const int64_t SE = (int64_t)S * FR_E;
+  float* __restrict__ X = Xall + (int64_t)mem * T * SE;
 
   // ---- weight pack staging (pieces [0, 9*256): QKV rows, [9*256, 12*256): Wout rows)
   u32x4 pf[FR_PIECES];
@@ -143,6 +145,11 @@ __global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ X
       for (int kp = 0; kp < NKP; ++kp)
         vfr[mt][kp] = cat8(va[mt][2 * kp], 2 * kp + 1 < NT ? va[mt][2 * kp + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
 
+#if defined(FR_DBG) && FR_DBG == 1  // diagnostics: no attention (O := Q)
+    bf16x8 of[NT];
+#pragma unroll
+    for (int qt = 0; qt < NT; ++qt) of[qt] = qf[qt] + kf[qt] + vfr[0][0];
+#else
     // ---- S^T[key][query] = K Q^T (scores already in log2 units), softmax over keys
     f32x4 st[NT][NT];
 #pragma unroll
@@ -190,6 +197,7 @@ __global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ X
     bf16x8 of[NT];
 #pragma unroll
     for (int qt = 0; qt < NT; ++qt) of[qt] = cat8(oa[0][qt], oa[1][qt], inv[qt]);
+#endif
 #pragma unroll
     for (int f = 0; f < FR_E / 16; ++f) {
       const bf16x8 wof = *(const bf16x8*)(wo + (16 * f + n) * FR_OUT_ST + 8 * g);
@@ -240,15 +248,16 @@ __global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ X
 
 }  // namespace
 
-hipError_t launch_feat_rows(float* X, const void* pack, int S, int T, int E, int H, float eps, hipStream_t st) {
-  if (S <= 0) return hipSuccess;
+hipError_t launch_feat_rows(float* X, const void* pack, int S, int T, int M, int E, int H, float eps,
+                            hipStream_t st) {
+  if (S <= 0 || M <= 0) return hipSuccess;
   if (E != FR_E || H != FR_H || T < 1 || T > 64) return hipErrorInvalidValue;
-  const dim3 grid((S + 3) / 4), block(256);
+  const dim3 grid((M * S + 3) / 4), block(256);
   const bf16* pk = (const bf16*)pack;
-  if (T <= 16) hipLaunchKernelGGL(feat_rows_kernel<1>, grid, block, 0, st, X, pk, S, T, eps);
-  else if (T <= 32) hipLaunchKernelGGL(feat_rows_kernel<2>, grid, block, 0, st, X, pk, S, T, eps);
-  else if (T <= 48) hipLaunchKernelGGL(feat_rows_kernel<3>, grid, block, 0, st, X, pk, S, T, eps);
-  else hipLaunchKernelGGL(feat_rows_kernel<4>, grid, block, 0, st, X, pk, S, T, eps);
+  if (T <= 16) hipLaunchKernelGGL(feat_rows_kernel<1>, grid, block, 0, st, X, pk, S, T, M, eps);
+  else if (T <= 32) hipLaunchKernelGGL(feat_rows_kernel<2>, grid, block, 0, st, X, pk, S, T, M, eps);
+  else if (T <= 48) hipLaunchKernelGGL(feat_rows_kernel<3>, grid, block, 0, st, X, pk, S, T, M, eps);
+  else hipLaunchKernelGGL(feat_rows_kernel<4>, grid, block, 0, st, X, pk, S, T, M, eps);
   return hipGetLastError();
 }
 

@@ -74,7 +74,8 @@ hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, float* 
 // 96 x 192 [Wq rows permuted & scaled by log2(e)/sqrt(32) | Wk rows permuted | Wv], then
 // 192 x 32 Wout[:, h*32 ..] with permuted columns
 constexpr int FEAT_PACK_HEAD = 96 * 192 + 192 * 32;
-hipError_t launch_feat_rows(float* X, const void* pack, int S, int T, int E, int H, float eps, hipStream_t st);
+// X holds M members [M][T][S][E]; one launch covers the M*S rows
+hipError_t launch_feat_rows(float* X, const void* pack, int S, int T, int M, int E, int H, float eps, hipStream_t st);
 
 // fused attention-between-features sublayer (bf16 only): X <- LN(X + MHA_feat(X)) per row,
 // wqkv [3*H*32][E] bf16, wout [E][H*32] bf16; rows per block = feat_block_rows(T) (0: unsupported T)

@@ -62,6 +62,7 @@ def target_uniques(y_train: np.ndarray) -> np.ndarray:
 
 
 DEFAULT_LANES = int(os.environ.get("MMPFN_LANES", "2"))  # concurrent member lanes of forward_many
+DEFAULT_BATCH = int(os.environ.get("MMPFN_BATCH", "2"))  # members per batched forward of forward_many
 
 
 class HipEngine:
@@ -99,6 +100,7 @@ class HipEngine:
         self._pos_cache: dict[int, torch.Tensor] = {}
         self._streams: list = []
         self.lanes = DEFAULT_LANES
+        self.batch = DEFAULT_BATCH
 
     # ------------------------------------------------------------------ plumbing
     def _stream(self) -> int:
@@ -186,7 +188,34 @@ class HipEngine:
             self.status()
         return out
 
-    def forward_many(self, items, precision: int, lanes: int | None = None) -> list[torch.Tensor]:
+    def forward_batch(self, items, precision: int) -> list[torch.Tensor]:
+        """Members of ONE geometry (same S, N, F and tokens) in one batched forward
+        (``mmpfn_forward_batch``: every layer kernel runs once over all members)."""
+        prep = [self._prepare(x, t, y) for x, t, y in items]
+        M = len(prep)
+        xd0, td, _, _, S, F, C, N, G = prep[0]
+        for p in prep[1:]:
+            if (p[4], p[5], p[6], p[7]) != (S, F, C, N):
+                raise ValueError("forward_batch members must share S, F, C and N")
+        if N < 1 or N > S:
+            raise ValueError(f"single_eval_pos must be in [1, {S}], got {N}")
+        pr = self._pos(G + C)
+        out = torch.empty((M, S - N, self.cfg.n_out), device=self.device, dtype=torch.float32)
+        arr = ctypes.c_void_p * M
+        xs = arr(*[_ptr(p[0]) for p in prep]) if F > 0 else None
+        ys = arr(*[_ptr(p[2]) for p in prep])
+        us = arr(*[_ptr(p[3]) for p in prep])
+        ns = (ctypes.c_int * M)(*[p[3].numel() for p in prep])
+        self._bind_stream()
+        self._check(
+            self.lib.mmpfn_forward_batch(self.ctx, M, xs, S, F, _ptr(td), C, ys, N, us, ns, _ptr(pr), _ptr(out),
+                                         precision),
+            "mmpfn_forward_batch",
+        )
+        return list(out.unbind(0))
+
+    def forward_many(self, items, precision: int, lanes: int | None = None,
+                     batch: int | None = None) -> list[torch.Tensor]:
         """Independent ensemble members ``[(x, tokens, y_train), ...]`` -> logits list.
 
         Members are spread over ``lanes`` forward lanes (per-member workspaces of the same
@@ -196,21 +225,41 @@ class HipEngine:
         do not depend on the lane count.
         """
         items = list(items)
+        batch = max(1, int(self.batch if batch is None else batch))
+        # work units: batches of up to `batch` members of one geometry, in member order
+        groups: dict = {}
+        for i, (x, t, y) in enumerate(items):
+            groups.setdefault(self._geometry(x, t, y), []).append(i)
+        units = []
+        for idx in groups.values():
+            units += [idx[j:j + batch] for j in range(0, len(idx), batch)]
+        units.sort(key=lambda u: u[0])
         if lanes is None:
             lanes = self.lanes
-        lanes = max(1, min(int(lanes), len(items), _lib.MMPFN_MAX_LANES))
+        lanes = max(1, min(int(lanes), len(units), _lib.MMPFN_MAX_LANES))
+        outs: list = [None] * len(items)
+
+        def run(unit):
+            if len(unit) == 1:
+                x, t, y = items[unit[0]]
+                outs[unit[0]] = self.forward(x, t, y, precision, check_nan=False)
+            else:
+                for i, o in zip(unit, self.forward_batch([items[i] for i in unit], precision)):
+                    outs[i] = o
+
         if lanes == 1:
-            return [self.forward(x, t, y, precision, check_nan=False) for x, t, y in items]
+            for u in units:
+                run(u)
+            return outs
         main = torch.cuda.current_stream(self.device)
         streams = self._lane_streams(lanes)
         for st in streams:
             st.wait_stream(main)
-        outs = []
         try:
-            for i, (x, t, y) in enumerate(items):
-                with torch.cuda.stream(streams[i % lanes]):
-                    self._check(self.lib.mmpfn_select_lane(self.ctx, i % lanes), "mmpfn_select_lane")
-                    outs.append(self.forward(x, t, y, precision, check_nan=False))
+            for k, u in enumerate(units):
+                with torch.cuda.stream(streams[k % lanes]):
+                    self._check(self.lib.mmpfn_select_lane(self.ctx, k % lanes), "mmpfn_select_lane")
+                    run(u)
         finally:
             self._check(self.lib.mmpfn_select_lane(self.ctx, 0), "mmpfn_select_lane")
             for st in streams:
@@ -218,6 +267,13 @@ class HipEngine:
         for o in outs:  # allocated on a lane stream, consumed on the caller's
             o.record_stream(main)
         return outs
+
+    def _geometry(self, x, tokens, y_train) -> tuple:
+        S = (x.shape[0] if x is not None else tokens.shape[0])
+        F = 0 if x is None else x.shape[-1]
+        C = 0 if tokens is None else tokens.shape[1]
+        N = int(np.asarray(y_train.shape if isinstance(y_train, torch.Tensor) else np.shape(y_train)).prod())
+        return (S, F, C, N, None if tokens is None else tokens.data_ptr())
 
     def _lane_streams(self, n: int) -> list:
         if len(self._streams) < n:

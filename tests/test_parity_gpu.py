@@ -250,9 +250,10 @@ def test_engine_deterministic_and_no_nan_at_pad_ufes_size():
     assert (a.argmax(-1) == c.argmax(-1)).float().mean() > 0.9
 
 
-@pytest.mark.parametrize("lanes", [2, 3])
-def test_forward_lanes_match_sequential(lanes):
-    """Members on concurrent lanes (own workspace + stream each) == one after another, bitwise."""
+@pytest.mark.parametrize("lanes,batch", [(2, 1), (3, 1), (1, 2), (1, 5), (2, 2), (2, 3)])
+def test_forward_lanes_match_sequential(lanes, batch):
+    """Members batched into one forward ([M][T][S][E] state) and/or on concurrent lanes (own
+    workspace + stream each) == one member after another, bitwise."""
     from synth import synth_image, synth_labels, synth_state_dict, synth_table
 
     from multimodalpfn_amd import _lib
@@ -274,8 +275,25 @@ def test_forward_lanes_match_sequential(lanes):
         ym = rng.permutation(3)[y.astype(np.int64)].astype(np.float32)
         items.append((xm, tok, ym))
     with torch.inference_mode():
-        seq = eng.forward_many(items, _lib.PREC_BF16, lanes=1)
-        par = eng.forward_many(items, _lib.PREC_BF16, lanes=lanes)
+        seq = eng.forward_many(items, _lib.PREC_BF16, lanes=1, batch=1)
+        par = eng.forward_many(items, _lib.PREC_BF16, lanes=lanes, batch=batch)
         eng.status()
     for a, b in zip(seq, par):
         assert torch.equal(a.cpu(), b.cpu())
+
+
+def test_forward_batch_fp32_matches_reference():
+    """fp32 parity mode through the batched forward (members stacked) against the goldens."""
+    from multimodalpfn_amd import _lib
+
+    z, meta, cfg, sd = load_case("pad_ufes_12l")
+    model = make_model(cfg, sd)
+    eng = model.engine()
+    tok = eng.mixer_tokens(torch.from_numpy(z["image"]).cuda(), _lib.PREC_F32)
+    item = (torch.from_numpy(z["x"]), tok, z["y_train"])
+    with torch.inference_mode():
+        outs = eng.forward_many([item, item, item], _lib.PREC_F32, lanes=1, batch=3)
+    for o in outs:
+        out = o.cpu().numpy()
+        assert rel_err(out, z["logits"]) <= F32_TOL
+        assert (out.argmax(1) == z["logits"].argmax(1)).all()
