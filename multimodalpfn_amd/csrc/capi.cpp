@@ -167,32 +167,36 @@ std::vector<float> pack_mlp2_perm(const std::vector<float>& w, int E, int Fh) {
   return o;
 }
 
-// featrow.hip weight pack, per head h (FEAT_PACK_HEAD floats):
-//   rows [0,32)  : Wq row 8*(r>>2 & 3) + 4*(r>>4) + (r&3) for r = 16f + rho -> head dim 8(rho>>2)+4f+(rho&3),
-//                  scaled by log2(e)/sqrt(32) (the feature-attention softmax scale, exp2 domain)
-//   rows [32,64) : Wk, same row permutation;   rows [64,96): Wv in natural order
-//   then [192][32] : Wout[e][h*32 + perm(c)], perm(8g+j) = j<4 ? 4g+j : 16+4g+(j-4)
+// featrow.hip weight pack (FEAT_PACK_LAYER floats, LDS images with FEAT_IMG_STRIDE-wide rows,
+// the 16 pad columns zero):
+//   per head h, rows [0,32) : Wq row 8(rho>>2) + 4f + (rho&3) for image row 16f + rho, scaled by
+//                             log2(e)/sqrt(32) (the feature-attention softmax scale, exp2 domain)
+//               rows [32,64): Wk, same row permutation;   rows [64,96): Wv in natural order
+//   then [192] rows of the out-projection: Wout[e][32h + perm(c)] at column 32h + c,
+//        perm(8g+j) = j<4 ? 4g+j : 16+4g+(j-4)
 // qkv: w_qkv [3][H][32][E] (multi_head_attention.py:423-430); wout_t: [E][H*32]
 std::vector<float> pack_feat_rows(const std::vector<float>& qkv, const std::vector<float>& wout_t, int H, int E) {
   const float c = 1.4426950408889634f / std::sqrt(32.0f);
-  std::vector<float> o((size_t)H * FEAT_PACK_HEAD);
+  const int ST = FEAT_IMG_STRIDE;
+  std::vector<float> o((size_t)FEAT_PACK_LAYER, 0.0f);
   for (int h = 0; h < H; ++h) {
-    float* ph = o.data() + (size_t)h * FEAT_PACK_HEAD;
+    float* ph = o.data() + (size_t)h * 96 * ST;
     for (int r = 0; r < 96; ++r) {
       const int j = r / 32, rr = r % 32, f = rr >> 4, rho = rr & 15;
       const int dd = j < 2 ? 8 * (rho >> 2) + 4 * f + (rho & 3) : rr;
       const float sc = j == 0 ? c : 1.0f;
       const float* src = qkv.data() + ((size_t)(j * H + h) * 32 + dd) * E;
-      for (int k = 0; k < E; ++k) ph[(size_t)r * E + k] = src[k] * sc;
+      for (int k = 0; k < E; ++k) ph[(size_t)r * ST + k] = src[k] * sc;
     }
-    float* po = ph + 96 * E;
-    for (int e = 0; e < E; ++e)
+  }
+  float* po = o.data() + (size_t)H * 96 * ST;
+  for (int e = 0; e < E; ++e)
+    for (int h = 0; h < H; ++h)
       for (int cc = 0; cc < 32; ++cc) {
         const int g = cc >> 3, jj = cc & 7;
         const int dd = jj < 4 ? 4 * g + jj : 16 + 4 * g + (jj - 4);
-        po[(size_t)e * 32 + cc] = wout_t[(size_t)e * H * 32 + h * 32 + dd];
+        po[(size_t)e * ST + 32 * h + cc] = wout_t[(size_t)e * H * 32 + h * 32 + dd];
       }
-  }
   return o;
 }
 

@@ -12,15 +12,18 @@
 //                      tiles concatenate into the A operand V^T[d][keys] of O^T = V^T P^T, in the
 //                      same permuted key order as P^T taken from the S^T accumulators
 //   O^T tiles         lane holds O^T[d 16mt+4g+i][query n]; concatenated over mt they are the B
-//                      operand of Y^T += Wout_h . O^T with Wout's 32 head columns permuted alike
+//                      operand (K-step h) of Y^T = Wout . O^T with Wout's columns permuted alike;
+//                      the six heads' fragments are kept (6*NT regs) and the out-projection runs
+//                      once after the last head, so no 192-wide accumulator lives across heads
 //   Y^T accumulators  lane holds Y^T[feature 16f+4g+i][token n]: residual + LayerNorm per token
 //                      with the 48 features of a lane reduced across the 4 lane groups.
 // The softmax scale log2(e)/sqrt(32) is folded into Wq (exp2 on the scores).
-// Only the weights move: per head one 48 KB pack (96 x 192 QKV slice + 192 x 32 Wout slice,
-// capi.cpp pack_feat_rows) is staged in LDS for the block's 4 waves (4 rows), double
-// buffered, the next head's pack in flight during the current head.
-// Per row and head: 18*NT MFMAs for QKV, NT^2 for S^T, 2*NT*ceil(NT/2) for P.V, 12*NT for the
-// out-projection; HBM traffic = X read + X written once.
+// Only the weights move: they are stored as LDS images (capi.cpp pack_feat_rows: 416-B rows,
+// so conflict-free ds_read_b128) and copied global -> LDS by LDS-DMA (global_load_lds, 1 KB
+// per wave-instruction, no staging registers): per head a 39 KB QKV slice, double buffered,
+// the next head's in flight during the current head; the 78 KB out-projection image over both
+// buffers at the end.  80 KB of LDS and <= 256 VGPRs per 4-row block: two blocks per CU.
+// Per row: 6*(18*NT + NT^2 + 2*NT*ceil(NT/2)) + 72*NT MFMAs; HBM traffic = X read + written once.
 #include "common.h"
 #include "kernels.h"
 
@@ -28,14 +31,11 @@ namespace mmpfn {
 
 namespace {
 
-constexpr int FR_E = 192;                     // model width
-constexpr int FR_H = 6;                       // heads
-constexpr int FR_QKV_ST = FR_E + 16;          // LDS row stride (bf16) of the 96 x 192 QKV slice: 416 B
-constexpr int FR_OUT_ST = 48;                 // LDS row stride (bf16) of the 192 x 32 Wout slice: 96 B
-constexpr int FR_QKV_EL = 96 * FR_QKV_ST;     // 19968
-constexpr int FR_BUF_EL = FR_QKV_EL + FR_E * FR_OUT_ST;  // 29184 bf16 per buffer
-constexpr int FR_PIECES = FEAT_PACK_HEAD / 8 / 256;       // 16-B pieces per thread and head (12)
-constexpr int FR_QKV_PIECES = 96 * FR_E / 8 / 256;        // of which QKV (9)
+constexpr int FR_E = 192;                        // model width
+constexpr int FR_H = 6;                          // heads
+constexpr int FR_ST = FEAT_IMG_STRIDE;           // bf16 row stride of every LDS image (416 B)
+constexpr int FR_QKV_IMG = 96 * FR_ST;           // one head's QKV image: 19968 bf16 = 39 KB
+constexpr int FR_PIECES = FR_QKV_IMG * 2 / 1024; // 1-KB DMA pieces per QKV image (39)
 
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -48,10 +48,13 @@ __device__ __forceinline__ bf16x8 cat8(const f32x4& a, const f32x4& b, float s =
   return r;
 }
 
+typedef __attribute__((address_space(3))) void lds_void;
+
 template <int NT>
-__global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ Xall, const bf16* __restrict__ pack,
-                                                           int S, int T, int M, float eps) {
-  __shared__ __attribute__((aligned(16))) bf16 wbuf[2 * FR_BUF_EL];
+__global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* __restrict__ Xall,
+                                                                         const bf16* __restrict__ pack, int S, int T,
+                                                                         int M, float eps) {
+  __shared__ __attribute__((aligned(1024))) bf16 wbuf[2 * FR_QKV_IMG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
   const int row = blockIdx.x * 4 + wave;  // row over the batch: member row / S, table row row % S
@@ -61,28 +64,13 @@ __global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ X
   const int64_t SE = (int64_t)S * FR_E;
   float* __restrict__ X = Xall + (int64_t)mem * T * SE;
 
-  // ---- weight pack staging (pieces [0, 9*256): QKV rows, [9*256, 12*256): Wout rows)
-  u32x4 pf[FR_PIECES];
-  auto fetch = [&](int h) {
-    const bf16* src = pack + (int64_t)h * FEAT_PACK_HEAD;
-#pragma unroll
-    for (int j = 0; j < FR_PIECES; ++j) pf[j] = *(const u32x4*)(src + (tid + 256 * j) * 8);
-  };
-  auto stash = [&](int buf) {
-    bf16* b = wbuf + buf * FR_BUF_EL;
-#pragma unroll
-    for (int j = 0; j < FR_PIECES; ++j) {
-      const int e = (tid + 256 * j) * 8;
-      if (j < FR_QKV_PIECES) {
-        *(u32x4*)(b + (e / FR_E) * FR_QKV_ST + e % FR_E) = pf[j];
-      } else {
-        const int e2 = e - 96 * FR_E;
-        *(u32x4*)(b + FR_QKV_EL + (e2 >> 5) * FR_OUT_ST + (e2 & 31)) = pf[j];
-      }
-    }
+  // LDS-DMA of `pieces` KB from src (global) to dst (LDS), KB piece p by wave p % 4
+  auto dma = [&](const bf16* src, bf16* dst, int pieces) {
+    for (int p = wave; p < pieces; p += 4)
+      __builtin_amdgcn_global_load_lds(src + p * 512 + lane * 8, (lds_void*)(dst + p * 512), 16, 0, 0);
   };
 
-  fetch(0);
+  dma(pack, wbuf, FR_PIECES);  // head 0 -> buffer 0
   // ---- the row's tokens as bf16 fragments (padding tokens t >= T are zero)
   bf16x8 xf[NT][FR_E / 32];
 #pragma unroll
@@ -96,121 +84,123 @@ __global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ X
       xf[tt][ks] = cat8(lo, hi);
     }
   }
-  stash(0);
-  __syncthreads();
+  __syncthreads();  // (its vmcnt(0) retires the DMA too)
 
-  f32x4 y[FR_E / 16][NT];
+  bf16x8 of[FR_H][NT];  // O^T fragments of every head (K-step h of the out-projection)
 #pragma unroll
-  for (int f = 0; f < FR_E / 16; ++f)
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) y[f][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   for (int h = 0; h < FR_H; ++h) {
-    if (h + 1 < FR_H) fetch(h + 1);
-    const bf16* wq = wbuf + (h & 1) * FR_BUF_EL;  // [96][FR_QKV_ST]: Q (permuted) | K (permuted) | V
-    const bf16* wo = wq + FR_QKV_EL;              // [192][FR_OUT_ST]: Wout[:, head cols permuted]
+    if (h + 1 < FR_H) dma(pack + (h + 1) * FR_QKV_IMG, wbuf + ((h + 1) & 1) * FR_QKV_IMG, FR_PIECES);
+    else dma(pack + FR_H * FR_QKV_IMG, wbuf, FR_PIECES);  // out-projection image, first half (buffer 0 is free)
+    const bf16* wq = wbuf + (h & 1) * FR_QKV_IMG;  // [96][FR_ST]: Q (permuted) | K (permuted) | V
 
-    // ---- Q^T, K^T (C^T tiles) and V (C tiles) of the row, K = 192 in 6 steps
-    f32x4 qa[2][NT], ka[2][NT], va[2][NT];
+    // ---- Q^T, K^T (C^T tiles) of the row, K = 192 in 6 steps (V after, to bound live registers)
+    bf16x8 qf[NT], kf[NT];
+    {
+      f32x4 qa[2][NT], ka[2][NT];
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
+      for (int f = 0; f < 2; ++f)
 #pragma unroll
-      for (int tt = 0; tt < NT; ++tt) qa[f][tt] = ka[f][tt] = va[f][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int tt = 0; tt < NT; ++tt) qa[f][tt] = ka[f][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < FR_E / 32; ++ks) {
-      bf16x8 wqf[2], wkf[2], wvf[2];
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        wqf[f] = *(const bf16x8*)(wq + (16 * f + n) * FR_QKV_ST + 32 * ks + 8 * g);
-        wkf[f] = *(const bf16x8*)(wq + (32 + 16 * f + n) * FR_QKV_ST + 32 * ks + 8 * g);
-        wvf[f] = *(const bf16x8*)(wq + (64 + 16 * f + n) * FR_QKV_ST + 32 * ks + 8 * g);
-      }
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt)
+      for (int ks = 0; ks < FR_E / 32; ++ks) {
+        bf16x8 wqf[2], wkf[2];
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
-          qa[f][tt] = mfma16(wqf[f], xf[tt][ks], qa[f][tt]);
-          ka[f][tt] = mfma16(wkf[f], xf[tt][ks], ka[f][tt]);
-          va[f][tt] = mfma16(xf[tt][ks], wvf[f], va[f][tt]);
+          wqf[f] = *(const bf16x8*)(wq + (16 * f + n) * FR_ST + 32 * ks + 8 * g);
+          wkf[f] = *(const bf16x8*)(wq + (32 + 16 * f + n) * FR_ST + 32 * ks + 8 * g);
         }
-    }
-    bf16x8 qf[NT], kf[NT];
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) qf[tt] = cat8(qa[0][tt], qa[1][tt]), kf[tt] = cat8(ka[0][tt], ka[1][tt]);
+        for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            qa[f][tt] = mfma16(wqf[f], xf[tt][ks], qa[f][tt]);
+            ka[f][tt] = mfma16(wkf[f], xf[tt][ks], ka[f][tt]);
+          }
+      }
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) qf[tt] = cat8(qa[0][tt], qa[1][tt]), kf[tt] = cat8(ka[0][tt], ka[1][tt]);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // phases in order: bounds the live registers (2 waves / SIMD)
+    // ---- V (C tiles: lane = head dim, 4 consecutive tokens) -> V^T A fragments per key-tile pair
     constexpr int NKP = (NT + 1) / 2;  // key-tile pairs (K = 32 keys per P.V MFMA)
     bf16x8 vfr[2][NKP];
+    {
+      f32x4 va[2][NT];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+      for (int f = 0; f < 2; ++f)
 #pragma unroll
-      for (int kp = 0; kp < NKP; ++kp)
-        vfr[mt][kp] = cat8(va[mt][2 * kp], 2 * kp + 1 < NT ? va[mt][2 * kp + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
+        for (int tt = 0; tt < NT; ++tt) va[f][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < FR_E / 32; ++ks) {
+        bf16x8 wvf[2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f) wvf[f] = *(const bf16x8*)(wq + (64 + 16 * f + n) * FR_ST + 32 * ks + 8 * g);
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+          for (int f = 0; f < 2; ++f) va[f][tt] = mfma16(xf[tt][ks], wvf[f], va[f][tt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int kp = 0; kp < NKP; ++kp)
+          vfr[mt][kp] = cat8(va[mt][2 * kp], 2 * kp + 1 < NT ? va[mt][2 * kp + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+    __builtin_amdgcn_sched_barrier(0);
 
-#if defined(FR_DBG) && FR_DBG == 1  // diagnostics: no attention (O := Q)
-    bf16x8 of[NT];
-#pragma unroll
-    for (int qt = 0; qt < NT; ++qt) of[qt] = qf[qt] + kf[qt] + vfr[0][0];
-#else
-    // ---- S^T[key][query] = K Q^T (scores already in log2 units), softmax over keys
-    f32x4 st[NT][NT];
-#pragma unroll
-    for (int kt = 0; kt < NT; ++kt)
-#pragma unroll
-      for (int qt = 0; qt < NT; ++qt) st[kt][qt] = mfma16(kf[kt], qf[qt], f32x4{0.f, 0.f, 0.f, 0.f});
-    float inv[NT];
+    // ---- per query tile: S^T[key][query] = K Q^T (log2 units), softmax over keys, O^T = V^T P^T
 #pragma unroll
     for (int qt = 0; qt < NT; ++qt) {
+      f32x4 st[NT];
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) st[kt] = mfma16(kf[kt], qf[qt], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int i = 0; i < 4; ++i)  // only the last key tile holds padding keys (T > 16*(NT-1))
+        if (16 * (NT - 1) + 4 * g + i >= T) st[NT - 1][i] = -INFINITY;
       float m = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (16 * kt + 4 * g + i >= T) st[kt][qt][i] = -INFINITY;
-          m = fmaxf(m, st[kt][qt][i]);
-        }
+        for (int i = 0; i < 4; ++i) m = fmaxf(m, st[kt][i]);
       m = max_rows4(m);
       float sum = 0.f;
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float e = __builtin_amdgcn_exp2f(st[kt][qt][i] - m);
-          st[kt][qt][i] = e;
+          const float e = __builtin_amdgcn_exp2f(st[kt][i] - m);
+          st[kt][i] = e;
           sum += e;
         }
-      inv[qt] = __builtin_amdgcn_rcpf(sum_rows4(sum));
-    }
-    // ---- O^T[d][query] = V^T P^T (P^T from the S^T accumulators, same permuted key order)
-    f32x4 oa[2][NT];
+      const float inv = __builtin_amdgcn_rcpf(sum_rows4(sum));
+      f32x4 oa[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+      for (int kp = 0; kp < NKP; ++kp) {
+        const bf16x8 pb = cat8(st[2 * kp], 2 * kp + 1 < NT ? st[2 * kp + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-      for (int qt = 0; qt < NT; ++qt) oa[mt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kp = 0; kp < NKP; ++kp)
-#pragma unroll
-      for (int qt = 0; qt < NT; ++qt) {
-        const bf16x8 pb = cat8(st[2 * kp][qt], 2 * kp + 1 < NT ? st[2 * kp + 1][qt] : f32x4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) oa[mt][qt] = mfma16(vfr[mt][kp], pb, oa[mt][qt]);
+        for (int mt = 0; mt < 2; ++mt) oa[mt] = mfma16(vfr[mt][kp], pb, oa[mt]);
       }
-    // ---- Y^T += Wout_h . O^T (normalised O^T as the B operand)
-    bf16x8 of[NT];
-#pragma unroll
-    for (int qt = 0; qt < NT; ++qt) of[qt] = cat8(oa[0][qt], oa[1][qt], inv[qt]);
-#endif
-#pragma unroll
-    for (int f = 0; f < FR_E / 16; ++f) {
-      const bf16x8 wof = *(const bf16x8*)(wo + (16 * f + n) * FR_OUT_ST + 8 * g);
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) y[f][tt] = mfma16(wof, of[tt], y[f][tt]);
+      of[h][qt] = cat8(oa[0], oa[1], inv);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if (h + 1 < FR_H) stash((h + 1) & 1);  // the buffer head h-1 read; every wave passed that barrier
-    __syncthreads();
+    __syncthreads();  // DMA of the next image landed; this head's buffer is free
   }
+  // second half of the out-projection image (buffer 1, read by head 5 until the barrier above)
+  dma(pack + FR_H * FR_QKV_IMG + FR_QKV_IMG, wbuf + FR_QKV_IMG, FR_PIECES);
+  __syncthreads();
 
-  // ---- residual + LayerNorm per token (lane = token n of tile tt, 48 of its 192 features)
+  // ---- per token tile: Y^T = Wout . O^T over K = 192 (K-step h = head h), image [192][FR_ST],
+  //      then residual + LayerNorm per token (lane = token n, 48 of its 192 features)
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) {
+    f32x4 y[FR_E / 16];
+#pragma unroll
+    for (int f = 0; f < FR_E / 16; ++f) {
+      y[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < FR_H; ++h)
+        y[f] = mfma16(*(const bf16x8*)(wbuf + (16 * f + n) * FR_ST + 32 * h + 8 * g), of[h][tt], y[f]);
+    }
     const int t = 16 * tt + n;
     const bool valid = rowok && t < T;
     float* xr = X + (int64_t)(t < T ? t : 0) * SE + (int64_t)sr * FR_E + 4 * g;
@@ -220,8 +210,8 @@ __global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ X
       const f32x4 xv = *(const f32x4*)(xr + 16 * f);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        y[f][tt][i] += xv[i];
-        sm += y[f][tt][i];
+        y[f][i] += xv[i];
+        sm += y[f][i];
       }
     }
     const float mean = sum_rows4(sm) * (1.0f / FR_E);
@@ -230,7 +220,7 @@ __global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ X
     for (int f = 0; f < FR_E / 16; ++f)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float dl = y[f][tt][i] - mean;
+        const float dl = y[f][i] - mean;
         q += dl * dl;
       }
     const float rs = 1.0f / sqrtf(sum_rows4(q) * (1.0f / FR_E) + eps);
@@ -239,7 +229,7 @@ __global__ __launch_bounds__(256, 1) void feat_rows_kernel(float* __restrict__ X
       for (int f = 0; f < FR_E / 16; ++f) {
         f32x4 ov;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ov[i] = (y[f][tt][i] - mean) * rs;
+        for (int i = 0; i < 4; ++i) ov[i] = (y[f][i] - mean) * rs;
         *(f32x4*)(xr + 16 * f) = ov;
       }
     }

@@ -70,10 +70,11 @@ hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, in
 hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, float* X, float eps, hipStream_t st);
 
 // row-resident attention-between-features sublayer (bf16 only, featrow.hip): one wave per
-// table row, T <= 64 tokens; `pack` = per head FEAT_PACK_HEAD bf16 (capi.cpp pack_feat_rows):
-// 96 x 192 [Wq rows permuted & scaled by log2(e)/sqrt(32) | Wk rows permuted | Wv], then
-// 192 x 32 Wout[:, h*32 ..] with permuted columns
-constexpr int FEAT_PACK_HEAD = 96 * 192 + 192 * 32;
+// table row, T <= 64 tokens; `pack` (capi.cpp pack_feat_rows) = LDS images with 416-B rows:
+// per head [96][FEAT_IMG_STRIDE] (Wq rows permuted & scaled by log2(e)/sqrt(32) | Wk rows
+// permuted | Wv), then the out-projection [192][FEAT_IMG_STRIDE] with permuted head columns
+constexpr int FEAT_IMG_STRIDE = 208;
+constexpr int FEAT_PACK_LAYER = (6 * 96 + 192) * FEAT_IMG_STRIDE;
 // X holds M members [M][T][S][E]; one launch covers the M*S rows
 hipError_t launch_feat_rows(float* X, const void* pack, int S, int T, int M, int E, int H, float eps, hipStream_t st);
 
