@@ -32,7 +32,7 @@ struct DevBuf {
 struct LayerW {  // packed per layer, [N][K] row-major
   DevBuf feat_qkv, feat_out, item_qkv, item_qtest, item_out, mlp1, mlp2;  // fp32
   DevBuf feat_qkv_h, feat_out_h, item_qkv_h, item_qtest_h, item_out_h, mlp1_h, mlp2_h;  // bf16
-  DevBuf feat_pack_h;  // bf16, per head [permuted QKV slice | permuted Wout slice] (featrow.hip)
+  DevBuf feat_pack_h;  // bf16 LDS images of the feature-attention weights (featrow.hip)
 };
 
 uint16_t f2bf(float f) {  // round-to-nearest-even, NaN preserving

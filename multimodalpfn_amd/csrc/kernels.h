@@ -54,8 +54,8 @@ hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool ou
 hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M, int E, int Fh, float eps, int prec,
                             hipStream_t st);
 
-// row-resident MLP sublayer (bf16 only): W1 [Fh][E] bf16, W2 [E][Fh] bf16 in the permuted
-// hidden order of pack_mlp2_perm (capi.cpp); Fh % 32 == 0
+// row-resident MLP sublayer (bf16 only, mlp_rows.hip): W1 [Fh][E] bf16, W2 [E][Fh] bf16 in the
+// permuted hidden order of pack_mlp2_perm (capi.cpp); Fh % 32 == 0, E == 192
 hipError_t launch_mlp_rows(float* X, const void* W1, const void* W2perm, int64_t M, int E, int Fh, float eps,
                            hipStream_t st);
 

@@ -1,18 +1,19 @@
 // Row-resident MLP sublayer for gfx950 (bf16 performance mode):
 //   X <- LayerNorm(X + GELU(X W1^T) W2^T)           (mlp.py:93-104, layer.py:437-455)
 //
-// Each wave owns 32 rows for the whole sublayer and keeps them in registers:
+// Each wave owns 32 rows (tokens) for the whole sublayer and keeps them in registers:
 //   * its rows of X, as bf16 B-operand fragments (A^T), loaded once from HBM;
-//   * the hidden activations of the current 32-wide hidden chunk, computed
-//     transposed (H^T = W1c . A^T) so the accumulator of one 16x16 tile pair is,
-//     lane for lane, the B operand of the down projection (Y^T += W2c . H^T) once the
-//     chunk's K order is permuted (pos 8g+j <-> hidden 4g+j / 16+4g+j-4; W2 is stored
-//     in that order, see pack_mlp2_perm in capi.cpp);
+//   * the hidden activations of a 32-wide hidden chunk, computed transposed
+//     (H^T = W1c . A^T) so the accumulator of one 16x16 tile pair is, lane for lane, the B
+//     operand of the down projection (Y^T += W2c . H^T) once the chunk's K order is
+//     permuted (pos 8g+j <-> hidden 4g+j / 16+4g+j-4; W2 stored so, capi.cpp pack_mlp2_perm);
 //   * the 192 x 32 output accumulator Y^T, then residual + LayerNorm across lanes.
-// Only the weights move through LDS: a 128-row block (4 waves) shares each 32-wide
-// hidden chunk of W1 (32 x 192) and W2 (192 x 32), double buffered, one barrier per
-// chunk, so weight bytes per row are a quarter of a 32-row tiling and X is read once
-// and written once.
+// Software pipeline over hidden chunks c (branch-free body, last chunk peeled): GELU(H(c)) on
+// the VALU beside the MFMAs of H(c+1), then Y^T += W2c . GELU(H(c)); one barrier per chunk.
+// Only the weights move through LDS: a 128-row block (4 waves) shares each chunk; W1 of chunk
+// c+2 and W2 of chunk c+1 are loaded into registers during chunk c and written to their LDS
+// slots after it (two slots each, 62 KB per block: two blocks per CU).  LDS rows of 416 B
+// (W1) and 96 B (W2) keep the ds_read_b128 fragment reads conflict-free.
 #include "common.h"
 #include "kernels.h"
 
@@ -20,14 +21,15 @@ namespace mmpfn {
 
 namespace {
 
-constexpr int RE = 192;               // model width
-constexpr int RHC = 32;               // hidden chunk
-constexpr int RROWS = 128;            // rows per block (4 waves x 32)
-constexpr int W1ST = RE + 16;         // W1 chunk LDS row stride (bf16): 416 B (32 mod 64: conflict-free b128)
-constexpr int W2ST = RHC + 16;        // W2 chunk LDS row stride (bf16): 96 B
-constexpr int W1EL = RHC * W1ST;      // 6400
-constexpr int BUFEL = W1EL + RE * W2ST;  // 6656 + 9216 bf16 per buffer
-constexpr int PIECES = (RHC * RE + RE * RHC) / 8 / 256;  // 16-B pieces per thread per chunk (6)
+constexpr int RE = 192;                    // model width
+constexpr int RHC = 32;                    // hidden chunk
+constexpr int RROWS = 128;                 // rows per block (4 waves x 32)
+constexpr int W1ST = RE + 16;              // W1 chunk LDS row stride (bf16): 416 B
+constexpr int W2ST = RHC + 16;             // W2 chunk LDS row stride (bf16): 96 B
+constexpr int W1EL = RHC * W1ST;           // 6656
+constexpr int W2EL = RE * W2ST;            // 9216
+constexpr int P1 = RHC * RE / 8 / 256;     // 16-B W1 pieces per thread and chunk (3)
+constexpr int P2 = RE * RHC / 8 / 256;     // 16-B W2 pieces per thread and chunk (3)
 
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -35,41 +37,47 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 
 __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X, const bf16* __restrict__ W1,
                                                           const bf16* __restrict__ W2p, int M, int Fh, float eps) {
-  __shared__ __attribute__((aligned(16))) bf16 wbuf[2 * BUFEL];
+  __shared__ __attribute__((aligned(16))) bf16 w1s[2 * W1EL];
+  __shared__ __attribute__((aligned(16))) bf16 w2s[2 * W2EL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * RROWS + wave * 32;
   const int nchunks = Fh / RHC;
 
-  // chunk c pieces: [0, 768) W1 rows c*32.. (24 pieces of 16 B per row), [768, 1536) W2 rows (4 per row)
-  u32x4 pf[PIECES];
-  auto fetch = [&](int c) {
+  // register staging: piece p of W1 chunk c = row c*32 + p/24, 16-B column p%24;
+  // piece q of W2 chunk c = row q/4, 16-B column q%4 of the chunk's 32 permuted columns
+  u32x4 r1[P1], r2[P2];
+  auto fetch1 = [&](int c) {
 #pragma unroll
-    for (int j = 0; j < PIECES; ++j) {
+    for (int j = 0; j < P1; ++j) {
       const int p = tid + 256 * j;
-      if (j < PIECES / 2) {
-        pf[j] = *(const u32x4*)(W1 + (int64_t)(c * RHC + p / 24) * RE + (p % 24) * 8);
-      } else {
-        const int q = p - RHC * RE / 8;
-        pf[j] = *(const u32x4*)(W2p + (int64_t)(q >> 2) * Fh + c * RHC + (q & 3) * 8);
-      }
+      r1[j] = *(const u32x4*)(W1 + (int64_t)(c * RHC + p / 24) * RE + (p % 24) * 8);
     }
   };
-  auto stash = [&](int buf) {
-    bf16* b = wbuf + buf * BUFEL;
+  auto fetch2 = [&](int c) {
 #pragma unroll
-    for (int j = 0; j < PIECES; ++j) {
+    for (int j = 0; j < P2; ++j) {
+      const int q = tid + 256 * j;
+      r2[j] = *(const u32x4*)(W2p + (int64_t)(q >> 2) * Fh + c * RHC + (q & 3) * 8);
+    }
+  };
+  auto stash1 = [&](int slot) {
+#pragma unroll
+    for (int j = 0; j < P1; ++j) {
       const int p = tid + 256 * j;
-      if (j < PIECES / 2) {
-        *(u32x4*)(b + (p / 24) * W1ST + (p % 24) * 8) = pf[j];
-      } else {
-        const int q = p - RHC * RE / 8;
-        *(u32x4*)(b + W1EL + (q >> 2) * W2ST + (q & 3) * 8) = pf[j];
-      }
+      *(u32x4*)(w1s + slot * W1EL + (p / 24) * W1ST + (p % 24) * 8) = r1[j];
+    }
+  };
+  auto stash2 = [&](int slot) {
+#pragma unroll
+    for (int j = 0; j < P2; ++j) {
+      const int q = tid + 256 * j;
+      *(u32x4*)(w2s + slot * W2EL + (q >> 2) * W2ST + (q & 3) * 8) = r2[j];
     }
   };
 
-  fetch(0);
+  fetch1(0);
+  fetch2(0);
   // the wave's rows as A^T fragments: lane = row (tile tt, col fr), 8 consecutive features
   bf16x8 af[2][RE / 32];
 #pragma unroll
@@ -86,40 +94,44 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X,
       af[tt][ks] = b;
     }
   }
-  stash(0);
+  stash1(0);
+  stash2(0);
+  if (nchunks > 1) {
+    fetch1(1);
+    stash1(1);
+  }
   __syncthreads();
 
-  f32x4 y[RE / 16][2];
-#pragma unroll
-  for (int o = 0; o < RE / 16; ++o) y[o][0] = y[o][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int c = 0; c < nchunks; ++c) {
-    if (c + 1 < nchunks) fetch(c + 1);
-    const bf16* w1 = wbuf + (c & 1) * BUFEL;
-    const bf16* w2 = w1 + W1EL;
-    // H^T [32 hidden][32 rows] = W1c . A^T
-    f32x4 h[2][2];
+  // H^T [32 hidden][32 rows] = W1c . A^T  (W1c in LDS)
+  auto hmma = [&](const bf16* w1, f32x4 (&h)[2][2]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) h[i][0] = h[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // W1 fragments one k-step ahead of the MFMAs (sched barriers keep the reads early)
-    bf16x8 wa[2][2];
-#pragma unroll
-    for (int ht = 0; ht < 2; ++ht) wa[0][ht] = *(const bf16x8*)(w1 + (ht * 16 + fr) * W1ST + fg * 8);
 #pragma unroll
     for (int ks = 0; ks < RE / 32; ++ks) {
-      if (ks + 1 < RE / 32) {
+      bf16x8 wa[2];
 #pragma unroll
-        for (int ht = 0; ht < 2; ++ht)
-          wa[(ks + 1) & 1][ht] = *(const bf16x8*)(w1 + (ht * 16 + fr) * W1ST + (ks + 1) * 32 + fg * 8);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+      for (int ht = 0; ht < 2; ++ht) wa[ht] = *(const bf16x8*)(w1 + (ht * 16 + fr) * W1ST + ks * 32 + fg * 8);
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) h[ht][tt] = mfma16(wa[ks & 1][ht], af[tt][ks], h[ht][tt]);
+        for (int tt = 0; tt < 2; ++tt) h[ht][tt] = mfma16(wa[ht], af[tt][ks], h[ht][tt]);
     }
-    // GELU; the two hidden tiles' rows 4g..4g+3 form this lane's permuted K=32 B fragment
-    bf16x8 hb[2];
+  };
+  f32x4 y[RE / 16][2];
+#pragma unroll
+  for (int o = 0; o < RE / 16; ++o) y[o][0] = y[o][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 h[2][2];
+  hmma(w1s, h);
+
+  // one chunk: slots W1(c+1) in w1s[(c+1)&1], W2(c) in w2s[c&1]; W1(c+2) -> w1s[c&1] and
+  // W2(c+1) -> w2s[(c+1)&1], written after this chunk's reads; both slots were last read in
+  // chunk c-1 (or, for W1(0), right before chunk 0 -- hence the stash after the reads)
+  auto chunk = [&](int c, auto morec) {
+    constexpr bool MORE = decltype(morec)::value;  // a chunk c+1 exists
+    const bool f1 = c + 2 < nchunks;
+    if (f1) fetch1(c + 2);
+    if (MORE) fetch2(c + 1);
+    bf16x8 hb[2];  // GELU of chunk c (VALU) beside the up-projection MFMAs of chunk c+1
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
 #pragma unroll
@@ -128,27 +140,21 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X,
         hb[tt][4 + i] = (bf16)gelu_tanh_fast(h[1][tt][i]);
       }
     }
-    // Y^T [192][32 rows] += W2c(perm) . H^T
-    // W2 fragments in groups of 4 output tiles, the next group's reads issued first
-    bf16x8 wb[2][4];
+    if (MORE) hmma(w1s + ((c + 1) & 1) * W1EL, h);
+    // Y^T [192][32 rows] += W2c(perm) . GELU(H^T)
+    const bf16* w2 = w2s + (c & 1) * W2EL;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) wb[0][i] = *(const bf16x8*)(w2 + (i * 16 + fr) * W2ST + fg * 8);
+    for (int o = 0; o < RE / 16; ++o) {
+      const bf16x8 wb = *(const bf16x8*)(w2 + (o * 16 + fr) * W2ST + fg * 8);
 #pragma unroll
-    for (int og = 0; og < RE / 64; ++og) {
-      if (og + 1 < RE / 64) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          wb[(og + 1) & 1][i] = *(const bf16x8*)(w2 + (((og + 1) * 4 + i) * 16 + fr) * W2ST + fg * 8);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) y[og * 4 + i][tt] = mfma16(wb[og & 1][i], hb[tt], y[og * 4 + i][tt]);
+      for (int tt = 0; tt < 2; ++tt) y[o][tt] = mfma16(wb, hb[tt], y[o][tt]);
     }
-    if (c + 1 < nchunks) stash((c + 1) & 1);
+    if (f1) stash1(c & 1);
+    if (MORE) stash2((c + 1) & 1);
     __syncthreads();
-  }
+  };
+  for (int c = 0; c + 1 < nchunks; ++c) chunk(c, std::true_type{});
+  chunk(nchunks - 1, std::false_type{});
 
   // residual + LayerNorm: lane = row, 48 of its 192 features (rows 16o + 4g + i of Y^T)
 #pragma unroll
