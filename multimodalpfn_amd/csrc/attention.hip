@@ -289,8 +289,12 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
         }
       }
     }
+#ifndef A2_NOSTAGE
     if (it + 1 < ntiles) lstore((it + 1) & 1);
+#endif
+#ifndef A2_NOSYNC
     __syncthreads();
+#endif
   };
 
   gload(0, std::bool_constant<true>{});  // masking is a no-op unless the tile is partial
@@ -415,7 +419,10 @@ __device__ __attribute__((noinline)) void a1_exact_rows(const Attn2Args& p, cons
   }
 }
 
-__global__ __launch_bounds__(256, A2_NCH == 2 ? 2 : 3) void attn_item2_kernel(const Attn2Args p) {
+#ifndef A2_OCC
+#define A2_OCC (A2_NCH == 2 ? 2 : 3)  // waves per SIMD the register budget targets
+#endif
+__global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args p) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2][2 * 4096];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -524,8 +531,12 @@ __global__ __launch_bounds__(256, A2_NCH == 2 ? 2 : 3) void attn_item2_kernel(co
     constexpr bool MASK = decltype(maskc)::value;
     constexpr bool FIRST = decltype(firstc)::value;
     const int k0 = it * A2_KT;
+#ifndef A2_NOSTAGE
     if (it + 1 < ntiles) gload(k0 + A2_KT, partial && it + 2 == ntiles);
     const unsigned char* Ks = lds[it & 1];
+#else
+    const unsigned char* Ks = lds[0];
+#endif
     if (active) {
       bf16x8 kf[2][2], vf[2][2];
 #pragma unroll
@@ -576,13 +587,23 @@ __global__ __launch_bounds__(256, A2_NCH == 2 ? 2 : 3) void attn_item2_kernel(co
           for (int sp = 0; sp < 2; ++sp) {
             bf16x8 pb;
 #pragma unroll
+#ifndef A2_NOEXP
             for (int j = 0; j < 8; ++j) pb[j] = (bf16)__builtin_amdgcn_exp2f(s[qb][u][8 * sp + j]);
+#else
+            for (int j = 0; j < 8; ++j) pb[j] = (bf16)s[qb][u][8 * sp + j];
+#endif
             o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[u][sp], pb, o[qb], 0, 0, 0);
+#ifndef A2_NOSEL
             lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[qb], 0, 0, 0);
+#endif
           }
     }
+#ifndef A2_NOSTAGE
     if (it + 1 < ntiles) lstore((it + 1) & 1);
+#endif
+#ifndef A2_NOSYNC
     __syncthreads();
+#endif
   };
 
   gload(0, ntiles == 1 && partial);

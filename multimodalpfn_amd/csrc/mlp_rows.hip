@@ -23,7 +23,6 @@ namespace {
 
 constexpr int RE = 192;                    // model width
 constexpr int RHC = 32;                    // hidden chunk
-constexpr int RROWS = 128;                 // rows per block (4 waves x 32)
 constexpr int W1ST = RE + 16;              // W1 chunk LDS row stride (bf16): 416 B
 constexpr int W2ST = RHC + 16;             // W2 chunk LDS row stride (bf16): 96 B
 constexpr int W1EL = RHC * W1ST;           // 6656
@@ -35,13 +34,20 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-__global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X, const bf16* __restrict__ W1,
-                                                          const bf16* __restrict__ W2p, int M, int Fh, float eps) {
+// TT = 16-row tiles per wave: 2 (32 rows, two waves per SIMD, accumulators in VGPRs) or 4 (64 rows,
+// one wave per SIMD with the 192 x 64 Y^T accumulator in AGPRs -- half the LDS weight reads per row,
+// but measured 15% slower: one wave cannot hide the LDS / GELU latency the second wave covers)
+template <int TT>
+__global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* __restrict__ X,
+                                                                       const bf16* __restrict__ W1,
+                                                                       const bf16* __restrict__ W2p, int M, int Fh,
+                                                                       float eps) {
+  constexpr int RROWS = 4 * 16 * TT;  // rows per block
   __shared__ __attribute__((aligned(16))) bf16 w1s[2 * W1EL];
   __shared__ __attribute__((aligned(16))) bf16 w2s[2 * W2EL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const int64_t m0 = (int64_t)blockIdx.x * RROWS + wave * 32;
+  const int64_t m0 = (int64_t)blockIdx.x * RROWS + wave * 16 * TT;
   const int nchunks = Fh / RHC;
 
   // register staging: piece p of W1 chunk c = row c*32 + p/24, 16-B column p%24;
@@ -79,9 +85,9 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X,
   fetch1(0);
   fetch2(0);
   // the wave's rows as A^T fragments: lane = row (tile tt, col fr), 8 consecutive features
-  bf16x8 af[2][RE / 32];
+  bf16x8 af[TT][RE / 32];
 #pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {
+  for (int tt = 0; tt < TT; ++tt) {
     const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
     const float* xr = X + m * RE + fg * 8;
 #pragma unroll
@@ -102,10 +108,12 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X,
   }
   __syncthreads();
 
-  // H^T [32 hidden][32 rows] = W1c . A^T  (W1c in LDS)
-  auto hmma = [&](const bf16* w1, f32x4 (&h)[2][2]) {
+  // H^T [32 hidden][16 TT rows] = W1c . A^T  (W1c in LDS)
+  auto hmma = [&](const bf16* w1, f32x4 (&h)[2][TT]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) h[i][0] = h[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt) h[i][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < RE / 32; ++ks) {
       bf16x8 wa[2];
@@ -114,13 +122,15 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X,
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) h[ht][tt] = mfma16(wa[ht], af[tt][ks], h[ht][tt]);
+        for (int tt = 0; tt < TT; ++tt) h[ht][tt] = mfma16(wa[ht], af[tt][ks], h[ht][tt]);
     }
   };
-  f32x4 y[RE / 16][2];
+  f32x4 y[RE / 16][TT];
 #pragma unroll
-  for (int o = 0; o < RE / 16; ++o) y[o][0] = y[o][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 h[2][2];
+  for (int o = 0; o < RE / 16; ++o)
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) y[o][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 h[2][TT];
   hmma(w1s, h);
 
   // one chunk: slots W1(c+1) in w1s[(c+1)&1], W2(c) in w2s[c&1]; W1(c+2) -> w1s[c&1] and
@@ -128,16 +138,23 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X,
   // chunk c-1 (or, for W1(0), right before chunk 0 -- hence the stash after the reads)
   auto chunk = [&](int c, auto morec) {
     constexpr bool MORE = decltype(morec)::value;  // a chunk c+1 exists
+#ifndef MLP_NOSTAGE
     const bool f1 = c + 2 < nchunks;
     if (f1) fetch1(c + 2);
     if (MORE) fetch2(c + 1);
-    bf16x8 hb[2];  // GELU of chunk c (VALU) beside the up-projection MFMAs of chunk c+1
+#endif
+    bf16x8 hb[TT];  // GELU of chunk c (VALU) beside the up-projection MFMAs of chunk c+1
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
+    for (int tt = 0; tt < TT; ++tt) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+#ifndef MLP_NOGELU
         hb[tt][i] = (bf16)gelu_tanh_fast(h[0][tt][i]);
         hb[tt][4 + i] = (bf16)gelu_tanh_fast(h[1][tt][i]);
+#else
+        hb[tt][i] = (bf16)h[0][tt][i];
+        hb[tt][4 + i] = (bf16)h[1][tt][i];
+#endif
       }
     }
     if (MORE) hmma(w1s + ((c + 1) & 1) * W1EL, h);
@@ -147,18 +164,22 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(float* __restrict__ X,
     for (int o = 0; o < RE / 16; ++o) {
       const bf16x8 wb = *(const bf16x8*)(w2 + (o * 16 + fr) * W2ST + fg * 8);
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) y[o][tt] = mfma16(wb, hb[tt], y[o][tt]);
+      for (int tt = 0; tt < TT; ++tt) y[o][tt] = mfma16(wb, hb[tt], y[o][tt]);
     }
+#ifndef MLP_NOSTAGE
     if (f1) stash1(c & 1);
     if (MORE) stash2((c + 1) & 1);
+#endif
+#ifndef MLP_NOSYNC
     __syncthreads();
+#endif
   };
   for (int c = 0; c + 1 < nchunks; ++c) chunk(c, std::true_type{});
   chunk(nchunks - 1, std::false_type{});
 
   // residual + LayerNorm: lane = row, 48 of its 192 features (rows 16o + 4g + i of Y^T)
 #pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {
+  for (int tt = 0; tt < TT; ++tt) {
     const int64_t m = m0 + tt * 16 + fr;
     const bool valid = m < M;
     float* xr = X + (valid ? m : (int64_t)M - 1) * RE + fg * 4;
@@ -202,7 +223,11 @@ hipError_t launch_mlp_rows(float* X, const void* W1, const void* W2perm, int64_t
                            hipStream_t st) {
   if (M <= 0) return hipSuccess;
   if (E != RE || Fh % RHC != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(mlp_rows_kernel, dim3((unsigned)((M + RROWS - 1) / RROWS)), dim3(256), 0, st, X,
+#ifndef MLP_TT
+#define MLP_TT 2  // 4 measured slower: 202 vs 175 us per two-member launch
+#endif
+  constexpr int RROWS = 64 * MLP_TT;
+  hipLaunchKernelGGL(mlp_rows_kernel<MLP_TT>, dim3((unsigned)((M + RROWS - 1) / RROWS)), dim3(256), 0, st, X,
                      (const bf16*)W1, (const bf16*)W2perm, (int)M, Fh, eps);
   return hipGetLastError();
 }

@@ -4,6 +4,7 @@ Usage (on the GPU box):  rocprofv3 --pmc <counters> -d <dir> -o run --output-for
                               python3 tools_prof_forward.py [n_forwards]
 """
 
+import os
 import sys
 from pathlib import Path
 
@@ -34,8 +35,12 @@ def main():
     im = torch.from_numpy(synth_image(S, 1, 2)).cuda()
     y = synth_labels(S, 6, 2)[:N]
     tok = eng.mixer_tokens(im, _lib.PREC_BF16)
+    batch = int(os.environ.get("MMPFN_PROF_BATCH", "1"))  # members per batched forward
     for _ in range(n):
-        out = eng.forward(x, tok, y, _lib.PREC_BF16, check_nan=False)
+        if batch > 1:
+            out = eng.forward_batch([(x, tok, y)] * batch, _lib.PREC_BF16)[0]
+        else:
+            out = eng.forward(x, tok, y, _lib.PREC_BF16, check_nan=False)
     eng.status()
     torch.cuda.synchronize()
     print("ok", tuple(out.shape), float(out.abs().mean()))

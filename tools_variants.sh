@@ -9,7 +9,7 @@ if [ "$1" = build ]; then
   for spec in "$@"; do
     name=${spec%%:*}; flags=${spec#*:}
     extra=""; [ "$SRC" = attention ] && extra="-fno-honor-nans"
-    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form=1 $extra \
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 ${FORM--mllvm -amdgpu-mfma-vgpr-form=1} $extra \
       $flags -x hip -c $C/$SRC.hip -o /tmp/var_$name.o || exit 1
     objs=$(ls $C/build/*.o | grep -v "/$SRC.hip.o")
     /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o multimodalpfn_amd/libmmpfn_var_$name.so $objs /tmp/var_$name.o || exit 1
