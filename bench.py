@@ -122,13 +122,22 @@ def time_item_attention(eng, T, reps):
     ms = e0.elapsed_time(e1) / reps
     flops = 4.0 * T * (N + Q) * N * H * d  # train 4*T*N*N*E + test (MQA) 4*T*Q*N*E
     achieved = flops / (ms * 1e-3) / 1e12
+    # HBM bytes per launch: rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same launch shape
+    # (tools_attn_pmc.sh; counters cannot be read from inside the timed process)
+    traffic, pmc = None, ROOT / "profiles" / "r01" / "attn_item2_pmc.json"
+    if pmc.exists():
+        rec = json.loads(pmc.read_text())
+        if rec.get("shape") == {"T": T, "H": H, "d": d, "S": S, "N": N}:
+            traffic = rec["hbm_bytes_per_launch"]
     return {
         "bound": "mfma",
         "achieved": round(achieved, 1),
         "peak": BF16_PEAK_TFLOPS,
         "unit": "TFLOP/s",
         "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
-        "traffic": None,
+        "traffic": traffic,
+        "traffic_unit": "bytes per launch (HBM, PMC: 2 x FETCH_SIZE + WRITE_SIZE, profiles/r01/attn_item2_pmc.json)",
+        "algorithmic_bytes": 2 * T * H * d * (S + 2 * N) + 2 * T * S * H * d,
         "kernel": "attn_item2_kernel (sample-axis attention, train + test-MQA rows of one layer per launch)",
         "per_launch_ms": round(ms, 4),
         "per_launch_flop": flops,
