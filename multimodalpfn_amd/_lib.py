@@ -83,7 +83,7 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     if _LIB is not None and path is None:
         return _LIB
     # MMPFN_LIB: diagnostics only (e.g. the stamps build of `make dbg`)
-    p = Path(path) if path is not None else Path(os.environ.get("MMPFN_LIB", str(LIB_PATH)))
+    p = Path(path) if path is not None else Path(os.environ.get("MMPFN_LIB") or str(LIB_PATH))
     if not p.exists():
         raise RuntimeError(
             f"MMPFN HIP engine library not found at {p}; build it with "

@@ -4,10 +4,9 @@
 //           K [b][h][pos][32] (Npad rows) and V^T [b][h][32][Npad]  (layer.py:341-372);
 //   * RES_LN : X <- LayerNorm(X + O . Wout^T)  (layer.py:437-455, no affine).
 // K is the model width (192): a wave keeps its 32 rows as bf16 fragments in registers
-// for the whole kernel and the block (4 waves, 128 rows) stages one 192 x 192 weight
-// panel at a time in LDS (row stride 416 B: conflict-free ds_read_b128), so each
-// output panel is one barrier and 144 v_mfma_f32_16x16x32_bf16 per wave.  Q and K
-// panels are computed transposed (lane = row, 4 consecutive head dims -> one 8-byte
+// for the whole kernel; the block (4 waves, 128 rows) streams the weights through LDS
+// (row stride 416 B: conflict-free ds_read_b128) -- QKV in 64-feature chunks, RES_LN as
+// one 192 x 192 panel.  Q and K chunks are computed transposed (lane = row, 4 consecutive head dims -> one 8-byte
 // store); the V panel is computed untransposed (lane = head dim, 4 consecutive rows
 // -> one 8-byte store into V^T).  The RES_LN panel keeps Y^T in registers and does the
 // residual + LayerNorm across lanes (in-register permlane reductions).
@@ -122,42 +121,71 @@ __device__ __forceinline__ void panel_mma(const bf16* Ws, const bf16x8 (&af)[2][
   }
 }
 
-// one output panel per block: grid = panels x row tiles, ordered so the panels of one row
-// tile are consecutive ids on one XCD (the rows come from HBM once, then from that L2)
-__global__ __launch_bounds__(256, 2) void rowgemm_qkv_kernel(const RgArgs p, int npanels) {
-  __shared__ __attribute__((aligned(16))) bf16 Ws[GE * WST];
+// QKV v2: one block per 128-row tile computes ALL N outputs (576: q|k|v, or 192: q), so X comes
+// from HBM once.  W streams through LDS in 64-feature chunks (two slots, 53 KB); chunk c+2 is fetched into registers while chunk c's MFMAs run and chunk c+1 is written to
+// its slot at the top of the iteration (its slot was last read before the previous barrier).
+constexpr int QC = 64;                     // output features per chunk
+constexpr int QCEL = QC * WST;             // chunk slot elements
+constexpr int QCP = QC * GE / 8 / 256;     // 16-B pieces per thread and chunk (6)
+
+__global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p) {
+  __shared__ __attribute__((aligned(16))) bf16 Ws[2 * QCEL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  int j, tile;
-  {
-    const int nb = gridDim.x, pid = blockIdx.x;
-    const int xcd = pid & 7, slot = pid >> 3;
-    const int lid = xcd * (nb >> 3) + min(xcd, nb & 7) + slot;
-    j = lid % npanels;
-    tile = lid / npanels;
-  }
-  const int64_t m0 = (int64_t)tile * GROWS + wave * 32;
-  stage_panel(p.W, j * GE, Ws, tid);
+  const int64_t m0 = (int64_t)blockIdx.x * GROWS + wave * 32;
+  const int nch = p.N / QC;
+  u32x4 r[QCP];
+  auto fetch = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < QCP; ++j) {
+      const int i = tid + 256 * j;
+      r[j] = *(const u32x4*)(p.W + (int64_t)(c * QC + i / (GE / 8)) * GE + (i % (GE / 8)) * 8);
+    }
+  };
+  auto stash = [&](int slot) {
+#pragma unroll
+    for (int j = 0; j < QCP; ++j) {
+      const int i = tid + 256 * j;
+      *(u32x4*)(Ws + slot * QCEL + (i / (GE / 8)) * WST + (i % (GE / 8)) * 8) = r[j];
+    }
+  };
+  fetch(0);
   bf16x8 af[2][GE / 32];
   load_rows<true>(p, m0, fr, fg, af);
-  f32x4 acc[GE / 16][2];
+  stash(0);
+  if (nch > 1) fetch(1);
   __syncthreads();
-  {
+  int rd = (int)p.a_rdiv;
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) stash((c + 1) & 1);
+    if (c + 2 < nch) fetch(c + 2);
+    const bf16* W = Ws + (c & 1) * QCEL;
+    const int n0 = c * QC, j = n0 / GE;  // 0 q, 1 k, 2 v
+    f32x4 acc[QC / 16][2];
+#pragma unroll
+    for (int f = 0; f < QC / 16; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (j < 2) {
-      panel_mma<true>(Ws, af, fr, fg, acc);
-      // C^T: lane = row m (tile tt, col fr); rows of the tile = features 16f + 4fg + i
+#pragma unroll
+      for (int ks = 0; ks < GE / 32; ++ks) {
+        bf16x8 w[QC / 16];
+#pragma unroll
+        for (int f = 0; f < QC / 16; ++f) w[f] = *(const bf16x8*)(W + (f * 16 + fr) * WST + ks * 32 + fg * 8);
+#pragma unroll
+        for (int f = 0; f < QC / 16; ++f)
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) acc[f][tt] = mfma16(w[f], af[tt][ks], acc[f][tt]);
+      }
+      // C^T: lane = row m (tile tt, col fr); rows of the tile = features n0 + 16f + 4fg + i
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         const int m = (int)(m0 + tt * 16 + fr);
         if (m >= p.M) continue;
-        int rd = (int)p.a_rdiv;
-        asm volatile("" : "+v"(rd));  // keep the scatter address math here (not hoisted to kernel entry)
         const int b = m / rd, pos = (int)p.a_roff + (m - b * rd);
         bf16* base = j == 0 ? p.q + ((int64_t)b * p.H * p.S + pos) * 32 : p.k + ((int64_t)b * p.H * p.Npad + pos) * 32;
         const int64_t hstride = (int64_t)(j == 0 ? p.S : p.Npad) * 32;
 #pragma unroll
-        for (int f = 0; f < GE / 16; ++f) {
-          const int n = f * 16 + fg * 4;  // 4 consecutive features, one head (32 | n)
+        for (int f = 0; f < QC / 16; ++f) {
+          const int n = (n0 - j * GE) + f * 16 + fg * 4;  // 4 consecutive features of one head
           bf16x4 o;
           o[0] = (bf16)acc[f][tt][0], o[1] = (bf16)acc[f][tt][1];
           o[2] = (bf16)acc[f][tt][2], o[3] = (bf16)acc[f][tt][3];
@@ -165,19 +193,26 @@ __global__ __launch_bounds__(256, 2) void rowgemm_qkv_kernel(const RgArgs p, int
         }
       }
     } else {
-      panel_mma<false>(Ws, af, fr, fg, acc);
+#pragma unroll
+      for (int ks = 0; ks < GE / 32; ++ks) {
+        bf16x8 w[QC / 16];
+#pragma unroll
+        for (int f = 0; f < QC / 16; ++f) w[f] = *(const bf16x8*)(W + (f * 16 + fr) * WST + ks * 32 + fg * 8);
+#pragma unroll
+        for (int f = 0; f < QC / 16; ++f)
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) acc[f][tt] = mfma16(af[tt][ks], w[f], acc[f][tt]);
+      }
       // C: lane = feature n (tile f, col fr); rows of the tile = rows m0 + 16tt + 4fg + i
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         const int ma = (int)(m0 + tt * 16 + fg * 4);
         if (ma >= p.M) continue;
-        int rd = (int)p.a_rdiv;
-        asm volatile("" : "+v"(rd));
         const int b = ma / rd, pos = (int)p.a_roff + (ma - b * rd);
         const bool whole = ma + 3 < p.M && (ma - b * rd) + 3 < rd && (pos & 3) == 0;
 #pragma unroll
-        for (int f = 0; f < GE / 16; ++f) {
-          const int n = f * 16 + fr;
+        for (int f = 0; f < QC / 16; ++f) {
+          const int n = (n0 - 2 * GE) + f * 16 + fr;
           if (whole) {
             bf16x4 o;
             o[0] = (bf16)acc[f][tt][0], o[1] = (bf16)acc[f][tt][1];
@@ -196,6 +231,7 @@ __global__ __launch_bounds__(256, 2) void rowgemm_qkv_kernel(const RgArgs p, int
         }
       }
     }
+    __syncthreads();
   }
 }
 
@@ -261,8 +297,7 @@ hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, in
   a.A = X, a.a_rdiv = a_rdiv, a.a_rmul = a_rmul, a.a_rmul2 = a_rmul2, a.a_roff = a_roff;
   a.W = (const bf16*)W, a.M = M, a.N = N;
   a.q = (bf16*)q, a.k = (bf16*)k, a.vt = (bf16*)vt, a.S = S, a.Npad = Npad, a.H = H;
-  const int npanels = N / GE;
-  hipLaunchKernelGGL(rowgemm_qkv_kernel, dim3(npanels * ((M + GROWS - 1) / GROWS)), dim3(256), 0, st, a, npanels);
+  hipLaunchKernelGGL(rowgemm_qkv2_kernel, dim3((M + GROWS - 1) / GROWS), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

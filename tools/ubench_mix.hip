@@ -59,7 +59,7 @@ void run() {
 
 int main() {
   run<4, 0, 0, 1>();
-  run<4, 0, 0, 2>();
   run<4, 0, 0, 4>();
+  run<4, 16, 8, 4>();
   return 0;
 }
