@@ -14,8 +14,8 @@ sum over members of (N + Q) / wall time, aggregated over all ranks (weak scaling
 for N > 1.
 
 Also reported: ``roofline`` of the dominant kernel (sample-axis attention, bf16
-MFMA; algorithmic flops 4*T*Nq*Nk*E per launch timed with HIP events on the
-engine stream) and ``cpu_baseline`` (the oracle's CPU restatement of the same
+MFMA; algorithmic flops 4*T*Nq*Nk*E per launch; every launch inside the timed region
+bracketed by HIP events on its lane stream, mmpfn_kernel_timing) and ``cpu_baseline`` (the oracle's CPU restatement of the same
 forward -- the reference's torch-SDPA branch -- on the host cores, bounded sample).
 """
 
@@ -86,6 +86,51 @@ def build_workload(device, world, members_per_gpu):
     return cfg, sd, model, x, y, image, members
 
 
+def attn_traffic(T):
+    """HBM bytes per attention launch over T token columns, from the committed PMC pass
+    (tools_attn_pmc.sh: rocprofv3 FETCH_SIZE and WRITE_SIZE runs at that launch shape)."""
+    H, d, S, N = 6, 32, S_ROWS, N_TRAIN
+    for pmc in sorted((ROOT / "profiles" / "r01").glob("attn_item2_pmc*.json")):
+        rec = json.loads(pmc.read_text())
+        if rec.get("shape") == {"T": T, "H": H, "d": d, "S": S, "N": N}:
+            return rec["hbm_bytes_per_launch"], str(pmc.relative_to(ROOT))
+    return None, None
+
+
+def live_roofline(lib, ctx, T_launch):
+    """Roofline of the dominant kernel from the launches INSIDE the timed region: HIP events
+    recorded by the engine on each lane's stream around every attn_item2 launch."""
+    import ctypes
+
+    ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+    assert lib.mmpfn_kernel_timing_read(ctx, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)) == 0
+    if n.value == 0:
+        return None
+    H, d, S, N = 6, 32, S_ROWS, N_TRAIN
+    per_ms, per_fl = ms.value / n.value, fl.value / n.value
+    uniform = abs(per_fl - 4.0 * T_launch * S * N * H * d) < 1.0
+    achieved = per_fl / (per_ms * 1e-3) / 1e12
+    traffic, src = attn_traffic(T_launch) if uniform else (None, None)
+    return {
+        "bound": "mfma",
+        "achieved": round(achieved, 1),
+        "peak": BF16_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
+        "traffic": traffic,
+        "traffic_unit": f"HBM bytes per launch (PMC: 2 x FETCH_SIZE + WRITE_SIZE, {src})" if src else None,
+        "algorithmic_bytes": 2 * T_launch * H * d * (S + 2 * N) + 2 * T_launch * S * H * d,
+        "kernel": "attn_item2_kernel (sample-axis attention: train + test-MQA rows of one layer, all members "
+                  "of a batched forward, per launch)",
+        "launches_timed": n.value,
+        "token_columns_per_launch": T_launch,
+        "per_launch_ms": round(per_ms, 4),
+        "per_launch_flop": per_fl,
+        "timing": "HIP events on the launching lane stream around every launch in the timed region "
+                  "(mmpfn_kernel_timing); lanes overlap, so a launch shares the GPU with the other lane's kernels",
+    }
+
+
 def time_item_attention(eng, T, reps):
     """Average launch duration of the sample-axis attention kernel at the workload's shape.
 
@@ -122,13 +167,7 @@ def time_item_attention(eng, T, reps):
     ms = e0.elapsed_time(e1) / reps
     flops = 4.0 * T * (N + Q) * N * H * d  # train 4*T*N*N*E + test (MQA) 4*T*Q*N*E
     achieved = flops / (ms * 1e-3) / 1e12
-    # HBM bytes per launch: rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same launch shape
-    # (tools_attn_pmc.sh; counters cannot be read from inside the timed process)
-    traffic, pmc = None, ROOT / "profiles" / "r01" / "attn_item2_pmc.json"
-    if pmc.exists():
-        rec = json.loads(pmc.read_text())
-        if rec.get("shape") == {"T": T, "H": H, "d": d, "S": S, "N": N}:
-            traffic = rec["hbm_bytes_per_launch"]
+    traffic, src = attn_traffic(T)
     return {
         "bound": "mfma",
         "achieved": round(achieved, 1),
@@ -136,7 +175,7 @@ def time_item_attention(eng, T, reps):
         "unit": "TFLOP/s",
         "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
         "traffic": traffic,
-        "traffic_unit": "bytes per launch (HBM, PMC: 2 x FETCH_SIZE + WRITE_SIZE, profiles/r01/attn_item2_pmc.json)",
+        "traffic_unit": f"HBM bytes per launch (PMC: 2 x FETCH_SIZE + WRITE_SIZE, {src})" if src else None,
         "algorithmic_bytes": 2 * T * H * d * (S + 2 * N) + 2 * T * S * H * d,
         "kernel": "attn_item2_kernel (sample-axis attention, train + test-MQA rows of one layer per launch)",
         "per_launch_ms": round(ms, 4),
@@ -259,6 +298,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    eng.lib.mmpfn_kernel_timing(eng.ctx, 1)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -266,6 +306,9 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    eng.lib.mmpfn_kernel_timing(eng.ctx, 0)
+    batch = eng.batch if args.batch is None else args.batch
+    live = live_roofline(eng.lib, eng.ctx, T * min(batch, len(mine))) if rank == 0 else None
     if world > 1:
         tt = torch.tensor([dt], device=device, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -279,7 +322,11 @@ def main():
             api = api_end_to_end(cfg, sd, x, y, image, M, prec == _lib.PREC_F32, args.api_steps, world)
         except Exception as e:  # noqa: BLE001 - reported, the headline number stands on its own
             api = {"error": f"{type(e).__name__}: {e}"}
-    roof = time_item_attention(eng, T, args.attn_reps) if rank == 0 else None
+    roof = None
+    if rank == 0:
+        iso = time_item_attention(eng, T, args.attn_reps)
+        roof = live if live is not None else iso
+        roof["isolated_single_member_launch"] = {k: iso[k] for k in ("achieved", "frac", "per_launch_ms", "traffic")}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sd, x, y, image)

@@ -152,6 +152,13 @@ int mmpfn_select_lane(mmpfn_ctx* ctx, int lane);
 int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
                                int T, int H, int Npad, int N);
 
+/* Measurement hook (no reference counterpart): while enabled, every sample-axis attention
+ * launch of the bf16 forward is bracketed by HIP events on its own stream.  enable=1 clears
+ * and starts a window, enable=0 stops it; _read synchronises and returns the summed launch
+ * durations, the launch count and their algorithmic flops (4*T*(N+Q)*N*E each). */
+int mmpfn_kernel_timing(mmpfn_ctx* ctx, int enable);
+int mmpfn_kernel_timing_read(mmpfn_ctx* ctx, double* total_ms, int64_t* launches, double* flops);
+
 #ifdef __cplusplus
 }
 #endif

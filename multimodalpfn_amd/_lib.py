@@ -72,6 +72,9 @@ SIGNATURES = [
     ("mmpfn_item_attention_layer", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i]),
     ("mmpfn_select_lane", _i, [_vp, _i]),
     ("mmpfn_forward_batch", _i, [_vp, _i, _vp, _i, _i, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _i]),
+    ("mmpfn_kernel_timing", _i, [_vp, _i]),
+    ("mmpfn_kernel_timing_read", _i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
+                                      ctypes.POINTER(ctypes.c_double)]),
 ]
 
 _LIB = None

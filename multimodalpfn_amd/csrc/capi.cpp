@@ -78,6 +78,12 @@ struct mmpfn_ctx {
   };
   std::vector<Lane> lanes;  // lanes[cur] is stale while cur is selected
   int cur = 0;
+  // live timing of the sample-axis attention launches (mmpfn_kernel_timing): HIP events
+  // recorded on the launching stream around every attn_item2 launch while enabled
+  bool kt_on = false;
+  std::vector<hipEvent_t> kt_pool;  // event pairs, reused across windows
+  size_t kt_used = 0;
+  double kt_flops = 0.0;
   template <typename A, typename B>
   static void swap_lane(A& a, B& b) {
     std::swap(a.ws_X, b.ws_X), std::swap(a.ws_O, b.ws_O), std::swap(a.ws_big, b.ws_big);
@@ -543,7 +549,22 @@ int run_layer(mmpfn_ctx* ctx, int l) {
       }
     }
     if (bf) {  // train rows (own heads) and test rows (head-0 K/V, MQA) in one launch
+      hipEvent_t* ev = nullptr;
+      if (ctx->kt_on) {
+        if (ctx->kt_used + 2 > ctx->kt_pool.size()) {
+          for (int i = 0; i < 64; ++i) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            ctx->kt_pool.push_back(e);
+          }
+        }
+        ev = &ctx->kt_pool[ctx->kt_used];
+        ctx->kt_used += 2;
+        ctx->kt_flops += 4.0 * TM * (double)(N + Q) * N * E;
+        HIPCHK(hipEventRecord(ev[0], st));
+      }
       HIPCHK(launch_attn_item2(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st));
+      if (ev) HIPCHK(hipEventRecord(ev[1], st));
     } else {
       HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, 0, N, N, -1, prec, st));
       if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, N, Q, N, 0, prec, st));
@@ -693,6 +714,8 @@ void mmpfn_destroy(mmpfn_ctx* ctx) {
   // teardown: errors here have no caller to report to
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  (void)hipDeviceSynchronize();  // lanes may still be running on other streams
+  for (hipEvent_t e : ctx->kt_pool) (void)hipEventDestroy(e);
   auto fr = [](DevBuf& b) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
@@ -881,6 +904,27 @@ int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const voi
     return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(launch_attn_item(q, k, vt, out, S, T, H, Npad, s0, nq, nk, kvh, precision, ctx->stream));
+  return MMPFN_OK;
+}
+
+int mmpfn_kernel_timing(mmpfn_ctx* ctx, int enable) {
+  if (!ctx) return MMPFN_ERR_INVALID;
+  if (enable) ctx->kt_used = 0, ctx->kt_flops = 0.0;
+  ctx->kt_on = enable != 0;
+  return MMPFN_OK;
+}
+
+int mmpfn_kernel_timing_read(mmpfn_ctx* ctx, double* total_ms, int64_t* launches, double* flops) {
+  if (!ctx || !total_ms || !launches || !flops) return MMPFN_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  double tot = 0.0;
+  for (size_t i = 0; i + 1 < ctx->kt_used; i += 2) {
+    HIPCHK(hipEventSynchronize(ctx->kt_pool[i + 1]));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->kt_pool[i], ctx->kt_pool[i + 1]));
+    tot += ms;
+  }
+  *total_ms = tot, *launches = (int64_t)(ctx->kt_used / 2), *flops = ctx->kt_flops;
   return MMPFN_OK;
 }
 

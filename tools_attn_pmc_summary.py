@@ -6,9 +6,10 @@ are all 16 B per lane, so the read bytes are 2 x FETCH_SIZE; WRITE_SIZE is exact
 stores' 64-B lines.  Output: one JSON object on stdout."""
 import csv
 import json
+import os
 import sys
 
-T, H, d, S, N = 36, 6, 32, 2298, 1838
+T, H, d, S, N = int(os.environ.get("ATT_T", 36)), 6, 32, 2298, 1838
 NPAD = (N + 63) // 64 * 64
 vals = {}
 for path in sys.argv[1:]:
