@@ -278,7 +278,7 @@ int finalize(mmpfn_ctx* ctx) {
     GETW(db1, "decoder_dict.standard.0.bias", (size_t)Fh);
     GETW(dw2, "decoder_dict.standard.2.weight", (size_t)d.n_out * Fh);
     GETW(db2, "decoder_dict.standard.2.bias", (size_t)d.n_out);
-    if ((rc = upload(ctx, ctx->dec_w1, *dw1, false))) return rc;
+    if ((rc = upload(ctx, ctx->dec_w1, transpose_out(*dw1, Fh, E), false))) return rc;  // [E][Fh]
     if ((rc = upload(ctx, ctx->dec_b1, *db1, false))) return rc;
     if ((rc = upload(ctx, ctx->dec_w2, *dw2, false))) return rc;
     if ((rc = upload(ctx, ctx->dec_b2, *db2, false))) return rc;

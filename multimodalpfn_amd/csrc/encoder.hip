@@ -48,7 +48,7 @@ __device__ Moments nan_moments(int n, Fn f, double* red) {
     }
   }
   sum = block_sum_d(sum, red);
-  cnt = block_sum_d(cnt, red + 4);
+  cnt = block_sum_d(cnt, red + 16);
   const double mu = sum / cnt;  // unclipped (torch_nanstd)
   double ss = 0.0;
   for (int s = threadIdx.x; s < n; s += blockDim.x) {
@@ -58,16 +58,18 @@ __device__ Moments nan_moments(int n, Fn f, double* red) {
       ss += dl * dl;
     }
   }
-  ss = block_sum_d(ss, red + 8);
+  ss = block_sum_d(ss, red + 32);
   Moments m;
   m.mean_clip = (float)(sum / (cnt < 1.0 ? 1.0 : cnt));
   m.std = (float)sqrt(ss / (cnt - 1.0));
   return m;
 }
 
-__global__ __launch_bounds__(256) void enc_x_stats_kernel(const float* __restrict__ x, int S, int F, int N, int fpg,
-                                                          int nf, float sigma, SlotParams* __restrict__ slots) {
-  __shared__ double red[16];
+// 1024 threads (16 waves): each pass over the rows is two strided loads per thread, so the
+// ~9 dependent passes per column are short; reduction slots of 16 waves at red + {0,16,32}
+__global__ __launch_bounds__(1024) void enc_x_stats_kernel(const float* __restrict__ x, int S, int F, int N, int fpg,
+                                                           int nf, float sigma, SlotParams* __restrict__ slots) {
+  __shared__ double red[48];
   __shared__ int s_cnt[8];
   const int g = blockIdx.x;
   // 1. constancy over all rows (RemoveEmptyFeatures) for each column of the group
@@ -88,9 +90,10 @@ __global__ __launch_bounds__(256) void enc_x_stats_kernel(const float* __restric
   }
   for (int k = nsel; k < fpg; ++k) src_of_slot[k] = -1;
 
-  int used = 0;
-  SlotParams sp[8];
-  for (int k = 0; k < fpg; ++k) {
+  // this block's slot (blockIdx.y): the slots of a group are independent once the group's
+  // constant columns are known; the embed kernel sums the groups' used flags
+  {
+    const int k = blockIdx.y;
     const int c = src_of_slot[k];
     SlotParams p;
     p.src = c;
@@ -113,7 +116,7 @@ __global__ __launch_bounds__(256) void enc_x_stats_kernel(const float* __restric
           }
         }
         sum = block_sum_d(sum, red);
-        cnt = block_sum_d(cnt, red + 4);
+        cnt = block_sum_d(cnt, red + 16);
         p.fill = (float)(sum / cnt);
       }
       const float fill = p.fill;
@@ -148,58 +151,77 @@ __global__ __launch_bounds__(256) void enc_x_stats_kernel(const float* __restric
       int eq = 0;
       for (int s = 1 + threadIdx.x; s < S; s += blockDim.x) eq += (normed(s) == u0);
       const double tot = block_sum_d((double)eq, red);
-      if ((int)(tot + 0.5) != S - 1) ++used;
+      p.scale = (int)(tot + 0.5) != S - 1 ? 1.f : 0.f;  // used flag; the embed kernel rescales
+    } else {
+      p.scale = 0.f;
     }
-    sp[k] = p;
+    if (threadIdx.x == 0) slots[g * fpg + k] = p;
   }
   (void)s_cnt;
-  const float scale = sqrtf((float)nf / (float)(used < 1 ? 1 : used));
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < fpg; ++k) {
-      sp[k].scale = scale;
-      slots[g * fpg + k] = sp[k];
-    }
-  }
 }
 
-// one thread per (token, 4 embedding columns)
+// EMB_TOK tokens per block: the per-token model inputs (u, NaN/inf indicators) are computed
+// once per (token, slot) into LDS next to the encoder weights and each token's
+// positional-embedding row; then one thread per (token, 4 embedding columns)
+// writes the embedding from LDS operands (contiguous 16-B stores over the block's tokens)
+constexpr int EMB_TOK = 16;
+constexpr int EMB_EMAX = 256;
 __global__ __launch_bounds__(256) void enc_x_embed_kernel(const float* __restrict__ x, int S, int F, int G, int fpg,
                                                           int nf, const SlotParams* __restrict__ slots,
                                                           const float* __restrict__ w, const float* __restrict__ pe,
                                                           float* __restrict__ X, int E, int* flag) {
+  __shared__ float su[EMB_TOK][8], si[EMB_TOK][8];
+  __shared__ float ws[EMB_EMAX * 16], ps[EMB_TOK][EMB_EMAX];
+  const int tid = threadIdx.x, nin = 2 * nf;
+  const int64_t ntok = (int64_t)S * G, tok0 = (int64_t)blockIdx.x * EMB_TOK;
+  for (int i = tid; i < E * nin; i += blockDim.x) ws[i] = w[i];
+  for (int i = tid; i < EMB_TOK * E; i += blockDim.x) {  // positional-embedding row of each token's group
+    const int t = i / E, e = i - t * E;
+    const int64_t tok = tok0 + t;
+    ps[t][e] = tok < ntok ? pe[(tok / S) * E + e] : 0.f;
+  }
+  if (tid < EMB_TOK * 8) {
+    const int i = tid >> 3, k = tid & 7;
+    const int64_t tok = tok0 + i;
+    float u = 0.f, ind = 0.f;
+    if (tok < ntok && k < fpg) {
+      const int g = (int)(tok / S), s = (int)(tok - (int64_t)g * S);
+      const SlotParams p = slots[g * fpg + k];
+      float used = 0.f;  // used-feature rescale sqrt(nf / used) of the group (encoders.py:608-655)
+      for (int j = 0; j < fpg; ++j) used += slots[g * fpg + j].scale;
+      const float scale = sqrtf((float)nf / fmaxf(used, 1.f));
+      if (p.src >= 0) {
+        const float raw = x[(int64_t)s * F + p.src];
+        ind = isnan(raw) ? -2.0f : (isinf(raw) ? (raw > 0 ? 2.0f : 4.0f) : 0.0f);
+        float v = bad(raw) ? p.fill : raw;
+        v = soft_clip_t(v, p.lo, p.hi);
+        v = tmin(tmax((v - p.mean) / p.sd, -100.f), 100.f);
+        u = v * scale;
+      }
+    }
+    su[i][k] = u, si[i][k] = ind;
+  }
+  __syncthreads();
   const int E4 = E / 4;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)S * G * E4) return;
-  const int e4 = idx % E4;
-  const int64_t tok = idx / E4;
-  const int s = tok % S, g = tok / S;
-  float u[8], ind[8];
-  for (int k = 0; k < nf; ++k) u[k] = ind[k] = 0.f;
-  for (int k = 0; k < fpg; ++k) {
-    const SlotParams p = slots[g * fpg + k];
-    if (p.src < 0) continue;
-    const float raw = x[(int64_t)s * F + p.src];
-    ind[k] = isnan(raw) ? -2.0f : (isinf(raw) ? (raw > 0 ? 2.0f : 4.0f) : 0.0f);
-    float v = bad(raw) ? p.fill : raw;
-    v = soft_clip_t(v, p.lo, p.hi);
-    v = tmin(tmax((v - p.mean) / p.sd, -100.f), 100.f);
-    u[k] = v * p.scale;
-  }
-  const int nin = 2 * nf;
-  f32x4 o;
   bool nan_seen = false;
+  for (int item = tid; item < EMB_TOK * E4; item += blockDim.x) {
+    const int i = item / E4, e4 = item - i * E4;
+    const int64_t tok = tok0 + i;
+    if (tok >= ntok) break;
+    f32x4 o;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int e = e4 * 4 + i;
-    const float* wr = w + e * nin;
-    float a = 0.f;
-    for (int k = 0; k < nf; ++k) a = fmaf(u[k], wr[k], a);
-    for (int k = 0; k < nf; ++k) a = fmaf(ind[k], wr[nf + k], a);
-    a += pe[g * E + e];
-    o[i] = a;
-    nan_seen |= isnan(a);
+    for (int c = 0; c < 4; ++c) {
+      const int e = e4 * 4 + c;
+      const float* wr = ws + e * nin;
+      float a = 0.f;
+      for (int k = 0; k < nf; ++k) a = fmaf(su[i][k], wr[k], a);
+      for (int k = 0; k < nf; ++k) a = fmaf(si[i][k], wr[nf + k], a);
+      a += ps[i][e];
+      o[c] = a;
+      nan_seen |= isnan(a);
+    }
+    *(f32x4*)(X + tok * E + e4 * 4) = o;
   }
-  *(f32x4*)(X + ((int64_t)g * S + s) * E + e4 * 4) = o;
   if (nan_seen) atomicOr(flag, 1);
 }
 
@@ -274,30 +296,69 @@ __global__ __launch_bounds__(256) void add_tokens_kernel(const float* __restrict
 }
 
 // decoder: Linear(E, Fh) + GELU + Linear(Fh, n_out) on one query row per block
-__global__ __launch_bounds__(256) void decoder_kernel(const float* __restrict__ X, const float* __restrict__ w1,
-                                                      const float* __restrict__ b1, int Fh,
-                                                      const float* __restrict__ w2, const float* __restrict__ b2,
-                                                      int n_out, float* __restrict__ out, int E) {
+// decoder MLP (transformer.py:388-403, 850-853): DEC_R query rows per block of 1024 threads.
+// W1 is stored transposed [E][Fh]: thread (kq, o) accumulates k in [kq*E/4, (kq+1)*E/4) for
+// hidden units o, o+256, o+512 with 16 loads in flight (coalesced rows, reused for all DEC_R
+// rows); the four k-quarter partials are summed in order through LDS.  The kernel is bound by
+// load latency (W1 is 0.6 MB per block), so the k split is what shortens it.
+constexpr int DEC_R = 4;
+constexpr int DEC_KQ = 4;
+__global__ __launch_bounds__(1024) void decoder_kernel(const float* __restrict__ X, int Q,
+                                                       const float* __restrict__ w1t,
+                                                       const float* __restrict__ b1, int Fh,
+                                                       const float* __restrict__ w2, const float* __restrict__ b2,
+                                                       int n_out, float* __restrict__ out, int E) {
   extern __shared__ float sm[];
-  float* xs = sm;       // [E]
-  float* hs = sm + E;   // [Fh]
-  const int q = blockIdx.x;
-  for (int i = threadIdx.x; i < E; i += blockDim.x) xs[i] = X[(int64_t)q * E + i];
-  __syncthreads();
-  for (int o = threadIdx.x; o < Fh; o += blockDim.x) {
-    const float* wr = w1 + (int64_t)o * E;
-    float a = 0.f;
-    for (int k = 0; k < E; ++k) a = fmaf(xs[k], wr[k], a);
-    hs[o] = gelu_erf(a + b1[o]);
+  float* xs = sm;                          // [DEC_R][E]
+  float* part = sm + DEC_R * E;            // [DEC_KQ][DEC_R][Fh]
+  float* hs = part;                        // [DEC_R][Fh], reuses quarter 0
+  const int q0 = blockIdx.x * DEC_R, tid = threadIdx.x;
+  for (int i = tid; i < DEC_R * E; i += blockDim.x) {
+    const int r = i / E;
+    xs[i] = q0 + r < Q ? X[(int64_t)(q0 + r) * E + (i - r * E)] : 0.f;
   }
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int o = wave; o < n_out; o += blockDim.x / 64) {
+  const int kq = tid >> 8, kw = E / DEC_KQ, kb = kq * kw;
+  for (int o = tid & 255; o < Fh; o += 256) {
+    float a[DEC_R];
+#pragma unroll
+    for (int r = 0; r < DEC_R; ++r) a[r] = 0.f;
+    int k = 0;
+    for (; k + 16 <= kw; k += 16) {
+      float w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = w1t[(int64_t)(kb + k + j) * Fh + o];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+#pragma unroll
+        for (int r = 0; r < DEC_R; ++r) a[r] = fmaf(xs[r * E + kb + k + j], w[j], a[r]);
+    }
+    for (; k < kw; ++k) {
+      const float w = w1t[(int64_t)(kb + k) * Fh + o];
+#pragma unroll
+      for (int r = 0; r < DEC_R; ++r) a[r] = fmaf(xs[r * E + kb + k], w, a[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < DEC_R; ++r) part[(kq * DEC_R + r) * Fh + o] = a[r];
+  }
+  __syncthreads();
+  for (int i = tid; i < DEC_R * Fh; i += blockDim.x) {
+    const int o = i % Fh;
+    float a = part[i];
+#pragma unroll
+    for (int j = 1; j < DEC_KQ; ++j) a += part[j * DEC_R * Fh + i];
+    hs[i] = gelu_erf(a + b1[o]);  // element i is read and written by this thread only
+  }
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int j = wave; j < DEC_R * n_out; j += blockDim.x / 64) {
+    const int r = j / n_out, o = j - r * n_out;
+    if (q0 + r >= Q) continue;
     const float* wr = w2 + (int64_t)o * Fh;
     float a = 0.f;
-    for (int k = lane; k < Fh; k += 64) a = fmaf(hs[k], wr[k], a);
+    for (int k = lane; k < Fh; k += 64) a = fmaf(hs[r * Fh + k], wr[k], a);
     a = wave_sum(a);
-    if (lane == 0) out[(int64_t)q * n_out + o] = a + b2[o];
+    if (lane == 0) out[(int64_t)(q0 + r) * n_out + o] = a + b2[o];
   }
 }
 
@@ -373,9 +434,10 @@ hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, 
                            hipStream_t st) {
   if (G <= 0) return hipSuccess;
   if (fpg > 8 || nf > 8 || nf < fpg) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(enc_x_stats_kernel, dim3(G), dim3(256), 0, st, x, S, F, N, fpg, nf, sigma, slots);
-  const int64_t n = (int64_t)S * G * (E / 4);
-  hipLaunchKernelGGL(enc_x_embed_kernel, dim3((n + 255) / 256), dim3(256), 0, st, x, S, F, G, fpg, nf, slots, w_enc,
+  hipLaunchKernelGGL(enc_x_stats_kernel, dim3(G, fpg), dim3(1024), 0, st, x, S, F, N, fpg, nf, sigma, slots);
+  if (fpg > 8 || nf > 8 || E > EMB_EMAX) return hipErrorInvalidValue;
+  const int64_t nblk = ((int64_t)S * G + EMB_TOK - 1) / EMB_TOK;
+  hipLaunchKernelGGL(enc_x_embed_kernel, dim3((unsigned)nblk), dim3(256), 0, st, x, S, F, G, fpg, nf, slots, w_enc,
                      posemb, X, E, flag);
   return hipGetLastError();
 }
@@ -404,11 +466,14 @@ hipError_t launch_add_tokens(const float* tok, int S, int C, const float* posemb
   return hipGetLastError();
 }
 
-hipError_t launch_decoder(const float* X, int Q, const float* w1, const float* b1, int Fh, const float* w2,
+hipError_t launch_decoder(const float* X, int Q, const float* w1t, const float* b1, int Fh, const float* w2,
                           const float* b2, int n_out, float* out, int E, hipStream_t st) {
   if (Q <= 0) return hipSuccess;
-  hipLaunchKernelGGL(decoder_kernel, dim3(Q), dim3(256), (E + Fh) * sizeof(float), st, X, w1, b1, Fh, w2, b2, n_out,
-                     out, E);
+  if (E % DEC_KQ) return hipErrorInvalidValue;
+  const size_t lds = (size_t)DEC_R * (E + DEC_KQ * Fh) * sizeof(float);  // 52 KB at E=192, Fh=768
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(decoder_kernel, dim3((Q + DEC_R - 1) / DEC_R), dim3(1024), lds, st, X, Q, w1t, b1, Fh, w2, b2,
+                     n_out, out, E);
   return hipGetLastError();
 }
 

@@ -114,7 +114,7 @@ struct SlotParams {  // per (group, slot): how to transform raw column -> model 
   float fill;        // NaN/inf replacement (train nanmean)
   float lo, hi;      // soft outlier bounds (or -inf/+inf when disabled)
   float mean, sd;    // train z-score (sd already includes the +1e-20)
-  float scale;       // sqrt(nf / used) for the group
+  float scale;       // 1 if the slot's column is used (non-constant after normalisation), else 0
 };
 hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, int nf, float sigma,
                            SlotParams* slots, const float* w_enc /*[E][2nf]*/, const float* posemb,
@@ -126,7 +126,7 @@ hipError_t launch_pos_emb(const float* rnd /*[n][E/4]*/, int n, const float* w /
                           const float* b, float* out /*[n][E]*/, int E, hipStream_t st);
 hipError_t launch_add_tokens(const float* tok /*[S][C][E]*/, int S, int C, const float* posemb /*[C][E]*/,
                              float* X /*[C][S][E] slice*/, int E, int* flag, hipStream_t st);
-hipError_t launch_decoder(const float* X /*[Q][E]*/, int Q, const float* w1, const float* b1, int Fh,
+hipError_t launch_decoder(const float* X /*[Q][E]*/, int Q, const float* w1t /*[E][Fh]*/, const float* b1, int Fh,
                           const float* w2, const float* b2, int n_out, float* out, int E, hipStream_t st);
 
 hipError_t launch_aggregate(const float* logits /*[M][Q][n_out]*/, int M, int Q, int n_out,
