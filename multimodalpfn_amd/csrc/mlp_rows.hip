@@ -114,15 +114,23 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt) h[i][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int PU = 2;  // k-steps of W1 fragments in flight ahead of their MFMAs (measured best of 1-3)
+    bf16x8 wa[PU][2];
+#pragma unroll
+    for (int i = 0; i < PU; ++i)
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht) wa[i][ht] = *(const bf16x8*)(w1 + (ht * 16 + fr) * W1ST + i * 32 + fg * 8);
 #pragma unroll
     for (int ks = 0; ks < RE / 32; ++ks) {
-      bf16x8 wa[2];
-#pragma unroll
-      for (int ht = 0; ht < 2; ++ht) wa[ht] = *(const bf16x8*)(w1 + (ht * 16 + fr) * W1ST + ks * 32 + fg * 8);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-        for (int tt = 0; tt < TT; ++tt) h[ht][tt] = mfma16(wa[ht], af[tt][ks], h[ht][tt]);
+        for (int tt = 0; tt < TT; ++tt) h[ht][tt] = mfma16(wa[ks % PU][ht], af[tt][ks], h[ht][tt]);
+      if (ks + PU < RE / 32)
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+          wa[ks % PU][ht] = *(const bf16x8*)(w1 + (ht * 16 + fr) * W1ST + (ks + PU) * 32 + fg * 8);
     }
   };
   f32x4 y[RE / 16][TT];
@@ -160,11 +168,18 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
     if (MORE) hmma(w1s + ((c + 1) & 1) * W1EL, h);
     // Y^T [192][32 rows] += W2c(perm) . GELU(H^T)
     const bf16* w2 = w2s + (c & 1) * W2EL;
+    {  // W2 fragments 4 tiles ahead of their MFMAs (fenced so the reads stay early; 3-6 measured)
+      constexpr int PF = 4;
+      bf16x8 wb[PF];
 #pragma unroll
-    for (int o = 0; o < RE / 16; ++o) {
-      const bf16x8 wb = *(const bf16x8*)(w2 + (o * 16 + fr) * W2ST + fg * 8);
+      for (int i = 0; i < PF; ++i) wb[i] = *(const bf16x8*)(w2 + (i * 16 + fr) * W2ST + fg * 8);
 #pragma unroll
-      for (int tt = 0; tt < TT; ++tt) y[o][tt] = mfma16(wb, hb[tt], y[o][tt]);
+      for (int o = 0; o < RE / 16; ++o) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt) y[o][tt] = mfma16(wb[o % PF], hb[tt], y[o][tt]);
+        if (o + PF < RE / 16) wb[o % PF] = *(const bf16x8*)(w2 + ((o + PF) * 16 + fr) * W2ST + fg * 8);
+      }
     }
 #ifndef MLP_NOSTAGE
     if (f1) stash1(c & 1);

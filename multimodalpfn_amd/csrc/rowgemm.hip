@@ -128,6 +128,33 @@ constexpr int QC = 64;                     // output features per chunk
 constexpr int QCEL = QC * WST;             // chunk slot elements
 constexpr int QCP = QC * GE / 8 / 256;     // 16-B pieces per thread and chunk (6)
 
+// acc[f][tt] over K = 192 for one 64-feature chunk in LDS: the next k-step's 4 fragments are
+// read before this k-step's 8 MFMAs (sched barrier keeps them early)
+template <bool TRANS>
+__device__ __forceinline__ void chunk_mma(const bf16* W, const bf16x8 (&af)[2][GE / 32], int fr, int fg,
+                                          f32x4 (&acc)[QC / 16][2]) {
+  bf16x8 w[2][QC / 16];
+#pragma unroll
+  for (int f = 0; f < QC / 16; ++f) w[0][f] = *(const bf16x8*)(W + (f * 16 + fr) * WST + fg * 8);
+#pragma unroll
+  for (int ks = 0; ks < GE / 32; ++ks) {
+    if (ks + 1 < GE / 32)
+#pragma unroll
+      for (int f = 0; f < QC / 16; ++f)
+        w[(ks + 1) & 1][f] = *(const bf16x8*)(W + (f * 16 + fr) * WST + (ks + 1) * 32 + fg * 8);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < QC / 16; ++f)
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        if constexpr (TRANS)
+          acc[f][tt] = mfma16(w[ks & 1][f], af[tt][ks], acc[f][tt]);
+        else
+          acc[f][tt] = mfma16(af[tt][ks], w[ks & 1][f], acc[f][tt]);
+      }
+  }
+}
+
 __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p) {
   __shared__ __attribute__((aligned(16))) bf16 Ws[2 * QCEL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -165,16 +192,7 @@ __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p) {
 #pragma unroll
     for (int f = 0; f < QC / 16; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (j < 2) {
-#pragma unroll
-      for (int ks = 0; ks < GE / 32; ++ks) {
-        bf16x8 w[QC / 16];
-#pragma unroll
-        for (int f = 0; f < QC / 16; ++f) w[f] = *(const bf16x8*)(W + (f * 16 + fr) * WST + ks * 32 + fg * 8);
-#pragma unroll
-        for (int f = 0; f < QC / 16; ++f)
-#pragma unroll
-          for (int tt = 0; tt < 2; ++tt) acc[f][tt] = mfma16(w[f], af[tt][ks], acc[f][tt]);
-      }
+      chunk_mma<true>(W, af, fr, fg, acc);
       // C^T: lane = row m (tile tt, col fr); rows of the tile = features n0 + 16f + 4fg + i
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
@@ -193,16 +211,7 @@ __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p) {
         }
       }
     } else {
-#pragma unroll
-      for (int ks = 0; ks < GE / 32; ++ks) {
-        bf16x8 w[QC / 16];
-#pragma unroll
-        for (int f = 0; f < QC / 16; ++f) w[f] = *(const bf16x8*)(W + (f * 16 + fr) * WST + ks * 32 + fg * 8);
-#pragma unroll
-        for (int f = 0; f < QC / 16; ++f)
-#pragma unroll
-          for (int tt = 0; tt < 2; ++tt) acc[f][tt] = mfma16(af[tt][ks], w[f], acc[f][tt]);
-      }
+      chunk_mma<false>(W, af, fr, fg, acc);
       // C: lane = feature n (tile f, col fr); rows of the tile = rows m0 + 16tt + 4fg + i
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
