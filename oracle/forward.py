@@ -104,7 +104,7 @@ def encode_x(spec: OracleSpec, w: dict, x: torch.Tensor, n_train: int) -> torch.
     fpg = spec.features_per_group
     pad = (fpg - Fdim % fpg) % fpg  # T/transformer.py:630-648
     if pad:
-        x = torch.cat([x, torch.zeros(S, pad, dtype=x.dtype)], 1)
+        x = torch.cat([x, torch.zeros(S, pad, dtype=x.dtype, device=x.device)], 1)
     G = x.shape[1] // fpg
     x = x.reshape(S, G, fpg)  # "s b (f n) -> s (b f) n" with b=1 (T/transformer.py:652-657,742)
 
@@ -151,7 +151,7 @@ def encode_x(spec: OracleSpec, w: dict, x: torch.Tensor, n_train: int) -> torch.
     nf = spec.encoder_features
     x = x * torch.sqrt(nf / used)
     if nf > fpg:  # VariableNumFeatures zero-padding of main and nan indicators
-        zp = torch.zeros(S, G, nf - fpg, dtype=x.dtype)
+        zp = torch.zeros(S, G, nf - fpg, dtype=x.dtype, device=x.device)
         x = torch.cat([x, zp], -1)
         ind = torch.cat([ind, zp], -1)
 
@@ -169,7 +169,7 @@ def encode_y(spec: OracleSpec, w: dict, y_train: torch.Tensor, S: int) -> torch.
     (T/encoders.py:954-974), Linear(2 -> E, bias).
     """
     N = y_train.shape[0]
-    y = torch.full((S,), float("nan"), dtype=y_train.dtype)
+    y = torch.full((S,), float("nan"), dtype=y_train.dtype, device=y_train.device)
     y[:N] = y_train
     mean = torch.nanmean(y[:N])
     ind = torch.isnan(y).to(y.dtype) * NAN_INDICATOR
@@ -272,7 +272,7 @@ def subspace_pos_emb(spec: OracleSpec, w: dict, n_tokens: int, dtype) -> torch.T
     if spec.model_seed:
         gen.manual_seed(spec.model_seed)
     r = torch.randn((n_tokens, spec.emsize // 4), generator=gen, dtype=torch.float32)
-    r = r.to(dtype)
+    r = r.to(dtype=dtype, device=w["feature_positional_embedding_embeddings.weight"].device)
     return _linear(r, w, "feature_positional_embedding_embeddings")
 
 

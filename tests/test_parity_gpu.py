@@ -297,3 +297,37 @@ def test_forward_batch_fp32_matches_reference():
         out = o.cpu().numpy()
         assert rel_err(out, z["logits"]) <= F32_TOL
         assert (out.argmax(1) == z["logits"].argmax(1)).all()
+
+
+@pytest.mark.parametrize(
+    "name,S,N,F,n_cls,seed",
+    [("B: 4096 support x 100 features, tabular", 5120, 4096, 100, 2, 1),
+     ("E: 10k support rows, long context", 12000, 10000, 20, 4, 4)],
+)
+def test_large_config_matches_oracle_on_device(name, S, N, F, n_cls, seed):
+    """BASELINE configs B and E at full size, tabular-only, 12 layers: the fp32 engine against
+    the oracle evaluated in fp32 on the same GPU (the checker's math moved to the device; it is
+    pinned by the reference goldens on CPU), and the bf16 engine's labels against fp32."""
+    from synth import synth_labels, synth_state_dict, synth_table
+
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    torch.backends.cuda.matmul.allow_tf32 = False
+    cfg = ModelConfig(mgm_heads=8, cap_heads=4)
+    sd = synth_state_dict(state_dict_spec(cfg), seed)
+    model = make_model(cfg, sd)
+    x = torch.from_numpy(synth_table(S, F, seed, nan_frac=0.01)).cuda()
+    y = torch.from_numpy(synth_labels(S, n_cls, seed)[:N]).cuda()
+    with torch.inference_mode():
+        f32 = model(None, x[:, None, :], None, y, single_eval_pos=N).squeeze(1).float().cpu().numpy()
+        with torch.autocast("cuda"):
+            b16 = model(None, x[:, None, :], None, y, single_eval_pos=N).squeeze(1).float().cpu().numpy()
+    w = {k: v.cuda() for k, v in torch_sd(sd).items()}
+    ref = oracle_forward(oracle_spec(cfg), w, x, None, y).cpu().numpy()
+    del w
+    torch.cuda.empty_cache()
+    assert np.isfinite(f32).all() and np.isfinite(b16).all()
+    assert rel_err(f32, ref) <= F32_TOL, (name, rel_err(f32, ref))
+    assert (f32.argmax(1) == ref.argmax(1)).all()
+    assert rel_err(b16, ref) <= BF16_TOL, (name, rel_err(b16, ref))
+    assert (b16.argmax(1) == ref.argmax(1)).mean() >= 0.9
