@@ -152,6 +152,27 @@ int mmpfn_select_lane(mmpfn_ctx* ctx, int lane);
 int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
                                int T, int H, int Npad, int N);
 
+/* Train-KV cache (fit_mode="fit_with_cache"), one per ensemble member.
+ * mmpfn_cache_build: forward of the N train rows only (x [N][F], tokens [N][C][E], y_train [N]);
+ *   keeps, per layer, head 0's K and V^T of the train rows -- the only K/V the test rows read
+ *   (multiquery item attention, layer.py:341-358; only_cache_first_head_kv, :362-372) -- and the
+ *   train statistics of the x / y encoders and the positional embeddings.  Replaces
+ *   InferenceEngineCacheKV.prepare's ens_model.forward(..., single_eval_pos=len(X))
+ *   (inference.py:425-436; cache_kv=True, multi_head_attention.py:461-472).
+ * mmpfn_cache_predict: Q test rows (x [Q][F], tokens [Q][C][E]) through the layers against the
+ *   cache (use_cached_kv, layer.py:344-358), logits [Q][n_out] in the cache's precision.  Replaces
+ *   iter_outputs' model(None, X_test, None, single_eval_pos=None) (inference.py:499-507).
+ * Equal to the test rows of a full forward over train + test rows, except that the x encoder's
+ * constant-column and used-feature tests see the train rows only (as the reference's cache).
+ * The cache belongs to the context that built it; free it with mmpfn_cache_free. */
+typedef struct mmpfn_cache mmpfn_cache;
+int mmpfn_cache_build(mmpfn_ctx* ctx, const float* x, int N, int F, const float* tokens, int C, const float* y_train,
+                      const float* uniq, int U, const float* pos_rand, int precision, mmpfn_cache** out);
+int mmpfn_cache_predict(mmpfn_ctx* ctx, const mmpfn_cache* cache, const float* x, int Q, int F, const float* tokens,
+                        int C, float* logits);
+int64_t mmpfn_cache_bytes(const mmpfn_cache* cache);
+void mmpfn_cache_free(mmpfn_ctx* ctx, mmpfn_cache* cache);
+
 /* Measurement hook (no reference counterpart): while enabled, every sample-axis attention
  * launch of the bf16 forward is bracketed by HIP events on its own stream.  enable=1 clears
  * and starts a window, enable=0 stops it; _read synchronises and returns the summed launch

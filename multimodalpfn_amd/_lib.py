@@ -72,6 +72,10 @@ SIGNATURES = [
     ("mmpfn_item_attention_layer", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i]),
     ("mmpfn_select_lane", _i, [_vp, _i]),
     ("mmpfn_forward_batch", _i, [_vp, _i, _vp, _i, _i, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _i]),
+    ("mmpfn_cache_build", _i, [_vp, _vp, _i, _i, _vp, _i, _vp, _vp, _i, _vp, _i, ctypes.POINTER(_vp)]),
+    ("mmpfn_cache_predict", _i, [_vp, _vp, _vp, _i, _i, _vp, _i, _vp]),
+    ("mmpfn_cache_bytes", _i64, [_vp]),
+    ("mmpfn_cache_free", None, [_vp, _vp]),
     ("mmpfn_kernel_timing", _i, [_vp, _i]),
     ("mmpfn_kernel_timing_read", _i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                       ctypes.POINTER(ctypes.c_double)]),

@@ -12,7 +12,7 @@ from typing import Any, Literal
 import torch
 
 from multimodalpfn_amd.constants import AUTOCAST_DTYPE_BYTE_SIZE, DEFAULT_DTYPE_BYTE_SIZE
-from multimodalpfn_amd.inference import InferenceEngineCachePreprocessing, InferenceEngineOnDemand
+from multimodalpfn_amd.inference import InferenceEngineCacheKV, InferenceEngineCachePreprocessing, InferenceEngineOnDemand
 from multimodalpfn_amd.utils import infer_fp16_inference_mode, load_model_criterion_config
 
 
@@ -88,6 +88,6 @@ def create_inference_engine(
     if fit_mode == "fit_preprocessors":
         return InferenceEngineCachePreprocessing.prepare(X_train, y_train, image_train, **common)
     if fit_mode == "fit_with_cache":
-        raise NotImplementedError("fit_mode='fit_with_cache' (train-KV cache) is not served yet; "
-                                  "use 'fit_preprocessors'")
+        return InferenceEngineCacheKV.prepare(X_train, y_train, image_train, device=device_,
+                                              autocast=use_autocast_, **common)
     raise ValueError(f"Invalid fit_mode: {fit_mode}")

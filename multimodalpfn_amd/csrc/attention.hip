@@ -383,6 +383,8 @@ struct Attn2Args {
   int b0, nb, kvb;     // shared-KV query rows (all heads) against kv head kvb
   int tasks_per_b, nblocks;
   int tstart[9];       // task prefix per kv head inside one column
+  int64_t kv_bstride;  // elements between the K (V^T) blocks of consecutive columns: H*Npad*32, or
+                       // Npad*32 for a head-0-only train-KV cache
 };
 
 __device__ __forceinline__ int a2_koff(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
@@ -443,7 +445,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
   const int jw = chunk * A2_QPB + wave * A2_QPW;  // first query of this wave
   const bool active = jw < cnt;               // wave-uniform
 
-  const int64_t kvoff = ((int64_t)b * p.H + g) * p.Npad * 32;
+  const int64_t kvoff = (int64_t)b * p.kv_bstride + (int64_t)g * p.Npad * 32;
   const bf16* Kg = p.k + kvoff;
   const bf16* Vg = p.vt + kvoff;
   const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
@@ -650,7 +652,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 }  // namespace
 
 hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
-                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st) {
+                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride) {
   if (na + nb <= 0 || T <= 0) return hipSuccess;
   if (nk <= 0 || Npad % A2_KT != 0 || nk > Npad || H > 8 || H <= 0) return hipErrorInvalidValue;
   if (nb > 0 && (kvb < 0 || kvb >= H)) return hipErrorInvalidValue;
@@ -658,6 +660,8 @@ hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void*
   a.q = (const bf16*)q, a.k = (const bf16*)k, a.vt = (const bf16*)vt, a.o = (bf16*)out;
   a.S = S, a.H = H, a.Npad = Npad, a.nk = nk;
   a.a0 = a0, a.na = na, a.b0 = b0, a.nb = nb, a.kvb = nb > 0 ? kvb : -1;
+  a.kv_bstride = kv_bstride > 0 ? kv_bstride : (int64_t)H * Npad * 32;
+  if (kv_bstride > 0 && (na > 0 || kvb != 0)) return hipErrorInvalidValue;  // cache layout holds head 0 only
   int acc = 0;
   for (int g = 0; g < H; ++g) {
     a.tstart[g] = acc;
@@ -688,16 +692,18 @@ hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int nw, hipStre
 }
 
 hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
-                            int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st) {
+                            int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st, int64_t kv_bstride) {
   AttnArgs a;
   a.q = q, a.k = k, a.vt = vt, a.o = out;
   a.q_bstride = (int64_t)H * S * 32, a.q_hstride = (int64_t)S * 32;
-  a.kv_bstride = (int64_t)H * Npad * 32, a.kv_hstride = (int64_t)Npad * 32, a.kpad = Npad;
+  a.kv_bstride = kv_bstride > 0 ? kv_bstride : (int64_t)H * Npad * 32, a.kv_hstride = (int64_t)Npad * 32;
+  a.kpad = Npad;
+  if (kv_bstride > 0 && kv_head_fixed != 0) return hipErrorInvalidValue;
   a.o_bstride = S, a.o_qstride = 1;
   a.s0 = s0, a.nq = nq, a.nk = nk, a.kvh_fixed = kv_head_fixed, a.H = H;
   if (prec == PREC_BF16) {
-    if (kv_head_fixed < 0) return launch_attn_item2(q, k, vt, out, S, T, H, Npad, nk, s0, nq, 0, 0, -1, st);
-    return launch_attn_item2(q, k, vt, out, S, T, H, Npad, nk, 0, 0, s0, nq, kv_head_fixed, st);
+    if (kv_head_fixed < 0) return launch_attn_item2(q, k, vt, out, S, T, H, Npad, nk, s0, nq, 0, 0, -1, st, kv_bstride);
+    return launch_attn_item2(q, k, vt, out, S, T, H, Npad, nk, 0, 0, s0, nq, kv_head_fixed, st, kv_bstride);
   }
   return launch_attn(a, T, prec, 4, st);
 }

@@ -45,6 +45,18 @@ uint16_t f2bf(float f) {  // round-to-nearest-even, NaN preserving
 
 }  // namespace
 
+// train-KV cache of one ensemble member (fit_mode="fit_with_cache"): per layer the head-0 K and
+// V^T of the train rows (all test rows read, layer.py:344-358), plus the train statistics of the
+// input encoders and the positional embeddings, so a predict runs only the test rows
+struct mmpfn_cache {
+  int N = 0, F = 0, G = 0, C = 0, T = 0, Npad = 0, prec = 0, U = 0;
+  DevBuf kv;     // [L][K: T x Npad x 32 | V^T: T x 32 x Npad], element size of prec
+  DevBuf slots;  // x-encoder SlotParams [G * fpg]
+  DevBuf ymean;  // y-encoder train nanmean
+  DevBuf uniq;   // sorted unique train labels [U]
+  DevBuf pe;     // positional embeddings [G + C][E]
+};
+
 struct mmpfn_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -80,6 +92,8 @@ struct mmpfn_ctx {
   int cur = 0;
   // live timing of the sample-axis attention launches (mmpfn_kernel_timing): HIP events
   // recorded on the launching stream around every attn_item2 launch while enabled
+  mmpfn_cache* cache_out = nullptr;       // being built by the current forward (train rows only)
+  const mmpfn_cache* cache_in = nullptr;  // used by the current forward (test rows only)
   bool kt_on = false;
   std::vector<hipEvent_t> kt_pool;  // event pairs, reused across windows
   size_t kt_used = 0;
@@ -473,6 +487,45 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
   return MMPFN_OK;
 }
 
+// test rows against a train-KV cache: every row of the state is a test row (N = 0), the encoders
+// apply the cached train statistics (transformer.py:779-784 use_cached_embeddings; encoders.py
+// steps with cache_trainset_representation)
+int embed_cached(mmpfn_ctx* ctx, const mmpfn_cache* cc, const float* x, int S, int F, const float* tokens, int C,
+                 int prec) {
+  const mmpfn_model_desc& d = ctx->d;
+  if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
+  if (S <= 0 || F != cc->F || C != cc->C || prec != cc->prec || (F > 0 && !x) || (C > 0 && !tokens))
+    return fail(ctx, MMPFN_ERR_INVALID, "test rows must match the cache's features, tokens and precision");
+  const int E = d.emsize, fpg = d.features_per_group, G = cc->G, T = cc->T;
+  const size_t R = (size_t)S * T;
+  hipStream_t st = ctx->stream;
+  ctx->S = S, ctx->T = T, ctx->N = 0, ctx->G = G, ctx->C = C, ctx->Npad = 0, ctx->prec = prec, ctx->M = 1;
+  RC(ensure(ctx, ctx->ws_X, R * E * 4));
+  RC(ensure(ctx, ctx->ws_O, R * E * 4));
+  const size_t Tpad = (T + 63) / 64 * 64;
+  RC(ensure(ctx, ctx->ws_big, (R * E + (size_t)2 * S * Tpad * E) * 4));
+  RC(ensure(ctx, ctx->ws_flag, 256));
+  int* flag = (int*)ctx->ws_flag.p;
+  HIPCHK(hipMemsetAsync(flag, 0, 4, st));
+  float* X = (float*)ctx->ws_X.p;
+  const float* pe = (const float*)cc->pe.p;
+  if (G)
+    HIPCHK(launch_encode_x(x, S, F, 0, G, fpg, d.encoder_features, d.outlier_sigma, (SlotParams*)cc->slots.p,
+                           (const float*)ctx->enc_w.p, pe, X, E, flag, st, false));
+  if (C) HIPCHK(launch_add_tokens(tokens, S, C, pe + (size_t)G * E, X + (size_t)G * S * E, E, flag, st));
+  HIPCHK(launch_encode_y(nullptr, 0, S, (const float*)cc->uniq.p, cc->U, (const float*)ctx->y_w.p,
+                         (const float*)ctx->y_b.p, X + (size_t)(T - 1) * S * E, E, (float*)cc->ymean.p, flag, st,
+                         false));
+  ctx->embedded = true;
+  return MMPFN_OK;
+}
+
+void cache_release(mmpfn_cache* cc) {
+  for (DevBuf* b : {&cc->kv, &cc->slots, &cc->ymean, &cc->uniq, &cc->pe})
+    if (b->p) (void)hipFree(b->p);
+  delete cc;
+}
+
 int run_layer(mmpfn_ctx* ctx, int l) {
   const mmpfn_model_desc& d = ctx->d;
   const LayerW& L = ctx->layers[l];
@@ -529,6 +582,27 @@ int run_layer(mmpfn_ctx* ctx, int l) {
     void* Qi = big;
     void* Ki = big + (size_t)RM * E * eb;
     void* Vi = (unsigned char*)Ki + (size_t)TM * H * Npad * 32 * eb;
+    if (ctx->cache_in) {  // every row is a test row: Q only, against the cached train K/V of head 0
+      const mmpfn_cache* cc = ctx->cache_in;
+      const size_t kvl = (size_t)T * cc->Npad * 32 * eb;
+      const unsigned char* Kc = (const unsigned char*)cc->kv.p + (size_t)l * 2 * kvl;
+      const unsigned char* Vc = Kc + kvl;
+      if (bf && E == 192) {
+        HIPCHK(launch_rowgemm_qkv(Xall, S, S, 1, 0, L.item_qtest_h.p, TM * S, E, Qi, Ki, Vi, S, Npad, H, st));
+      } else {
+        GemmArgs c = gargs();
+        c.A = Xall, c.lda = E, c.a_rdiv = S, c.a_rmul = S, c.a_roff = 0;
+        c.W = W(L.item_qtest, L.item_qtest_h, prec);
+        c.M = TM * S, c.N = E, c.K = E;
+        c.q = Qi, c.k = Ki, c.v = Vi, c.S = S, c.Npad = Npad, c.T = TM, c.H = H;
+        HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+      }
+      const int64_t cstride = (int64_t)cc->Npad * 32;
+      if (bf)
+        HIPCHK(launch_attn_item2(Qi, Kc, Vc, O, S, TM, H, cc->Npad, cc->N, 0, 0, 0, S, 0, st, cstride));
+      else
+        HIPCHK(launch_attn_item(Qi, Kc, Vc, O, S, TM, H, cc->Npad, 0, S, cc->N, 0, prec, st, cstride));
+    } else {
     if (bf && E == 192) {  // row-resident projections straight into the attention layouts
       HIPCHK(launch_rowgemm_qkv(Xall, N, S, 1, 0, L.item_qkv_h.p, TM * N, 3 * E, Qi, Ki, Vi, S, Npad, H, st));
       if (Q > 0)
@@ -547,6 +621,13 @@ int run_layer(mmpfn_ctx* ctx, int l) {
         c.M = TM * Q, c.N = E;
         HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
       }
+    }
+    if (ctx->cache_out) {  // keep head 0's K / V^T of every column (the test rows' KV, layer.py:344-358)
+      mmpfn_cache* cc = ctx->cache_out;
+      const size_t blk = (size_t)Npad * 32 * eb, kvl = (size_t)T * blk;
+      unsigned char* Kc = (unsigned char*)cc->kv.p + (size_t)l * 2 * kvl;
+      HIPCHK(hipMemcpy2DAsync(Kc, blk, Ki, (size_t)H * blk, blk, T, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpy2DAsync(Kc + kvl, blk, Vi, (size_t)H * blk, blk, T, hipMemcpyDeviceToDevice, st));
     }
     if (bf) {  // train rows (own heads) and test rows (head-0 K/V, MQA) in one launch
       hipEvent_t* ev = nullptr;
@@ -568,6 +649,7 @@ int run_layer(mmpfn_ctx* ctx, int l) {
     } else {
       HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, 0, N, N, -1, prec, st));
       if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, N, Q, N, 0, prec, st));
+    }
     }
     if (bf && E == 192) {
       HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, RM, Xall, d.ln_eps, st));
@@ -905,6 +987,82 @@ int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const voi
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(launch_attn_item(q, k, vt, out, S, T, H, Npad, s0, nq, nk, kvh, precision, ctx->stream));
   return MMPFN_OK;
+}
+
+int mmpfn_cache_build(mmpfn_ctx* ctx, const float* x, int N, int F, const float* tokens, int C, const float* y_train,
+                      const float* uniq, int U, const float* pos_rand, int precision, mmpfn_cache** out) {
+  if (!ctx || !out || !y_train || !uniq || !pos_rand) return MMPFN_ERR_INVALID;
+  *out = nullptr;
+  HIPCHK(hipSetDevice(ctx->device));
+  RC(embed(ctx, x, N, F, tokens, C, y_train, N, uniq, U, pos_rand, precision));
+  const mmpfn_model_desc& d = ctx->d;
+  const int E = d.emsize, fpg = d.features_per_group, eb = precision == PREC_BF16 ? 2 : 4;
+  mmpfn_cache* cc = new mmpfn_cache;
+  cc->N = N, cc->F = F, cc->G = ctx->G, cc->C = C, cc->T = ctx->T, cc->Npad = ctx->Npad, cc->prec = precision;
+  cc->U = U;
+  hipStream_t st = ctx->stream;
+  auto build = [&]() -> int {
+    RC(ensure(ctx, cc->kv, (size_t)d.nlayers * 2 * cc->T * cc->Npad * 32 * eb));
+    RC(ensure(ctx, cc->slots, (size_t)(cc->G + 1) * fpg * sizeof(SlotParams)));
+    RC(ensure(ctx, cc->ymean, 4));
+    RC(ensure(ctx, cc->uniq, (size_t)U * 4));
+    RC(ensure(ctx, cc->pe, (size_t)(cc->G + C + 1) * E * 4));
+    if (cc->G)
+      HIPCHK(hipMemcpyAsync(cc->slots.p, ctx->ws_slots.p, (size_t)cc->G * fpg * sizeof(SlotParams),
+                            hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(cc->ymean.p, ctx->ws_scr.p, 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(cc->uniq.p, uniq, (size_t)U * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(cc->pe.p, ctx->ws_pe.p, (size_t)(cc->G + C) * E * 4, hipMemcpyDeviceToDevice, st));
+    ctx->cache_out = cc;
+    for (int l = 0; l < d.nlayers; ++l) {
+      const int rc = run_layer(ctx, l);
+      if (rc) {
+        ctx->cache_out = nullptr;
+        return rc;
+      }
+    }
+    ctx->cache_out = nullptr;
+    return MMPFN_OK;
+  };
+  const int rc = build();
+  if (rc) {
+    (void)hipStreamSynchronize(st);
+    cache_release(cc);
+    return rc;
+  }
+  *out = cc;
+  return MMPFN_OK;
+}
+
+int mmpfn_cache_predict(mmpfn_ctx* ctx, const mmpfn_cache* cache, const float* x, int Q, int F, const float* tokens,
+                        int C, float* logits) {
+  if (!ctx || !cache || !logits) return MMPFN_ERR_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  RC(embed_cached(ctx, cache, x, Q, F, tokens, C, cache->prec));
+  ctx->cache_in = cache;
+  for (int l = 0; l < ctx->d.nlayers; ++l) {
+    const int rc = run_layer(ctx, l);
+    if (rc) {
+      ctx->cache_in = nullptr;
+      return rc;
+    }
+  }
+  ctx->cache_in = nullptr;
+  return decode(ctx, logits);
+}
+
+int64_t mmpfn_cache_bytes(const mmpfn_cache* cache) {
+  if (!cache) return 0;
+  return (int64_t)(cache->kv.bytes + cache->slots.bytes + cache->ymean.bytes + cache->uniq.bytes + cache->pe.bytes);
+}
+
+void mmpfn_cache_free(mmpfn_ctx* ctx, mmpfn_cache* cache) {
+  if (!cache) return;
+  if (ctx) {
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+  }
+  cache_release(cache);
 }
 
 int mmpfn_kernel_timing(mmpfn_ctx* ctx, int enable) {

@@ -431,10 +431,11 @@ hipError_t launch_aggregate(const float* logits, int M, int Q, int n_out, const 
 
 hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, int nf, float sigma,
                            SlotParams* slots, const float* w_enc, const float* posemb, float* X, int E, int* flag,
-                           hipStream_t st) {
+                           hipStream_t st, bool stats) {
   if (G <= 0) return hipSuccess;
   if (fpg > 8 || nf > 8 || nf < fpg) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(enc_x_stats_kernel, dim3(G, fpg), dim3(1024), 0, st, x, S, F, N, fpg, nf, sigma, slots);
+  if (stats)
+    hipLaunchKernelGGL(enc_x_stats_kernel, dim3(G, fpg), dim3(1024), 0, st, x, S, F, N, fpg, nf, sigma, slots);
   if (fpg > 8 || nf > 8 || E > EMB_EMAX) return hipErrorInvalidValue;
   const int64_t nblk = ((int64_t)S * G + EMB_TOK - 1) / EMB_TOK;
   hipLaunchKernelGGL(enc_x_embed_kernel, dim3((unsigned)nblk), dim3(256), 0, st, x, S, F, G, fpg, nf, slots, w_enc,
@@ -443,8 +444,8 @@ hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, 
 }
 
 hipError_t launch_encode_y(const float* y_train, int N, int S, const float* uniq, int U, const float* w,
-                           const float* b, float* Xy, int E, float* scratch, int* flag, hipStream_t st) {
-  hipLaunchKernelGGL(y_stats_kernel, dim3(1), dim3(256), 0, st, y_train, N, scratch);
+                           const float* b, float* Xy, int E, float* scratch, int* flag, hipStream_t st, bool stats) {
+  if (stats) hipLaunchKernelGGL(y_stats_kernel, dim3(1), dim3(256), 0, st, y_train, N, scratch);
   const int64_t n = (int64_t)S * (E / 4);
   hipLaunchKernelGGL(enc_y_embed_kernel, dim3((n + 255) / 256), dim3(256), 0, st, y_train, N, S, uniq, U, w, b,
                      scratch, Xy, E, flag);

@@ -101,12 +101,15 @@ struct AttnArgs {
 hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int waves_per_block, hipStream_t st);
 // bf16 sample-axis attention of one layer in one launch (attention.hip, attn_item2_kernel):
 //   own-head rows [a0, a0+na) of every head against that head's K/V, and rows [b0, b0+nb) of
-//   every head against K/V head kvb (nb = 0: none); keys [0, nk), Npad % 64 == 0
+//   every head against K/V head kvb (nb = 0: none); keys [0, nk), Npad % 64 == 0.
+//   kv_bstride > 0: K / V^T hold head 0 only, column blocks kv_bstride elements apart (train-KV
+//   cache; then na = 0 and kvb = 0)
 hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
-                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st);
+                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0);
 // item attention: queries s in [s0, s0+nq), keys [0, nk); kv_head_fixed >= 0 forces that KV head
 hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
-                            int Npad, int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st);
+                            int Npad, int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st,
+                            int64_t kv_bstride = 0);
 
 // ---- encoders / decoder ------------------------------------------------------------
 struct SlotParams {  // per (group, slot): how to transform raw column -> model input
@@ -118,10 +121,11 @@ struct SlotParams {  // per (group, slot): how to transform raw column -> model 
 };
 hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, int nf, float sigma,
                            SlotParams* slots, const float* w_enc /*[E][2nf]*/, const float* posemb,
-                           float* X /*[T][S][E]*/, int E, int* flag, hipStream_t st);
+                           float* X /*[T][S][E]*/, int E, int* flag, hipStream_t st, bool stats = true);
 hipError_t launch_encode_y(const float* y_train, int N, int S, const float* uniq, int U,
                            const float* w /*[E][2]*/, const float* b, float* Xy /*[S][E]*/, int E,
-                           float* scratch, int* flag, hipStream_t st);
+                           float* scratch, int* flag, hipStream_t st, bool stats = true);
+// stats = false: slots / scratch[0] already hold the train statistics (train-KV cache predict)
 hipError_t launch_pos_emb(const float* rnd /*[n][E/4]*/, int n, const float* w /*[E][E/4]*/,
                           const float* b, float* out /*[n][E]*/, int E, hipStream_t st);
 hipError_t launch_add_tokens(const float* tok /*[S][C][E]*/, int S, int C, const float* posemb /*[C][E]*/,

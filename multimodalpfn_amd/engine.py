@@ -188,6 +188,47 @@ class HipEngine:
             self.status()
         return out
 
+    # ------------------------------------------------------------------ train-KV cache
+    def cache_build(self, x, tokens, y_train, precision: int) -> "TrainCache":
+        """``fit_mode="fit_with_cache"``: forward the train rows once and keep, per layer, head 0's
+        K/V of the train rows plus the encoders' train statistics (``mmpfn_cache_build``;
+        reference ``InferenceEngineCacheKV.prepare``, inference.py:403-445)."""
+        xd, td, yd, uniq, S, F, C, N, G = self._prepare(x, tokens, y_train)
+        if N != S:
+            raise ValueError(f"cache_build takes the train rows only: {S} rows, {N} labels")
+        pr = self._pos(G + C)
+        h = ctypes.c_void_p()
+        self._bind_stream()
+        self._check(
+            self.lib.mmpfn_cache_build(self.ctx, _ptr(xd), N, F, _ptr(td), C, _ptr(yd), _ptr(uniq), uniq.numel(),
+                                       _ptr(pr), precision, ctypes.byref(h)),
+            "mmpfn_cache_build",
+        )
+        return TrainCache(self, h.value, N=N, F=F, C=C, precision=precision)
+
+    def cache_predict(self, cache: "TrainCache", x, tokens) -> torch.Tensor:
+        """Test rows against a train-KV cache: logits ``[Q, n_out]`` (``mmpfn_cache_predict``;
+        reference ``InferenceEngineCacheKV.iter_outputs``, inference.py:470-512)."""
+        if cache.engine is not self or not cache.handle:
+            raise ValueError("the cache belongs to another engine or was freed")
+        xd = None if x is None else self._dev(x)
+        if xd is not None and xd.dim() == 3:
+            xd = xd.reshape(xd.shape[0], xd.shape[-1])
+        td = None if tokens is None else self._dev(tokens)
+        Q = xd.shape[0] if xd is not None else td.shape[0]
+        F = xd.shape[1] if xd is not None else 0
+        C = td.shape[1] if td is not None else 0
+        if (F, C) != (cache.F, cache.C):
+            raise ValueError(f"test rows have F={F}, C={C}; the cache was built with F={cache.F}, C={cache.C}")
+        out = torch.empty((Q, self.cfg.n_out), device=self.device, dtype=torch.float32)
+        self._bind_stream()
+        self._check(
+            self.lib.mmpfn_cache_predict(self.ctx, ctypes.c_void_p(cache.handle), _ptr(xd), Q, F, _ptr(td), C,
+                                         _ptr(out)),
+            "mmpfn_cache_predict",
+        )
+        return out
+
     def forward_batch(self, items, precision: int) -> list[torch.Tensor]:
         """Members of ONE geometry (same S, N, F and tokens) in one batched forward
         (``mmpfn_forward_batch``: every layer kernel runs once over all members)."""
@@ -334,3 +375,26 @@ class HipEngine:
         self._bind_stream()
         self._check(self.lib.mmpfn_decode(self.ctx, _ptr(out)), "mmpfn_decode")
         return out
+
+
+class TrainCache:
+    """Device-resident train-KV cache of one ensemble member (owned by its engine's context)."""
+
+    def __init__(self, engine: HipEngine, handle: int, *, N: int, F: int, C: int, precision: int):
+        self.engine, self.handle = engine, handle
+        self.N, self.F, self.C, self.precision = N, F, C, precision
+
+    @property
+    def nbytes(self) -> int:
+        return int(self.engine.lib.mmpfn_cache_bytes(ctypes.c_void_p(self.handle))) if self.handle else 0
+
+    def free(self) -> None:
+        if self.handle and getattr(self.engine, "ctx", None):
+            self.engine.lib.mmpfn_cache_free(self.engine.ctx, ctypes.c_void_p(self.handle))
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass

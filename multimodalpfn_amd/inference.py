@@ -5,7 +5,9 @@ Mirror of ``mmpfn/models/mmpfn/inference.py``.  ``InferenceEngineCachePreprocess
 each member's preprocessing at ``fit`` and at ``predict`` transforms the test
 rows and runs one forward per member (``inference.py:217-351``);
 ``InferenceEngineOnDemand`` (``"low_memory"``) re-fits the preprocessing at every
-predict (``:73-213``).
+predict (``:73-213``); ``InferenceEngineCacheKV`` (``"fit_with_cache"``) runs the train rows
+through the model once at ``fit`` and keeps each member's train-KV cache on the device, so a
+predict forwards the test rows only (``:352-512``; unlike the reference it also serves images).
 
 MI355X-specific: the modality projection (MGM / CAP / MoE) depends only on the
 image rows, which every member shares, so it runs once per predict instead of
@@ -164,3 +166,68 @@ class InferenceEngineOnDemand(InferenceEngine):
                                  forced_dtype=self.force_inference_dtype, model=self.model)
         for out, m in zip(outs, members):
             yield out, m.config
+
+
+@dataclass
+class InferenceEngineCacheKV(InferenceEngine):
+    """``fit_mode="fit_with_cache"`` (``inference.py:352-512``): at ``fit`` every member's train rows
+    go through the model once and the engine keeps, on the device, head 0's K/V of the train rows
+    per layer plus the encoders' train statistics; a predict then forwards only the test rows
+    (``mmpfn_cache_build`` / ``mmpfn_cache_predict``).  The reference serves tabular inputs only
+    here (its prepare passes no image, ``:425-436``); images are served: the modality tokens of
+    the train rows are computed at fit and those of the test rows at predict (the mixers are
+    row-wise).  Precision is fixed at fit.  Members are sharded over ranks like the other engines.
+    """
+
+    caches: dict = field(default_factory=dict)
+    ensemble_configs: Sequence[Any] = ()
+    preprocessors: Sequence[Any] = ()
+    n_members: int = 0
+    model: Any = None
+    precision: int = _lib.PREC_F32
+    mine: list = field(default_factory=list)
+    gather: Any = None
+
+    @classmethod
+    def prepare(cls, X_train, y_train, image_train, *, cat_ix, model, ensemble_configs, n_workers, rng,
+                dtype_byte_size, force_inference_dtype, save_peak_mem, device, autocast) -> InferenceEngineCacheKV:
+        from multimodalpfn_amd.parallel import member_shard
+
+        itr = fit_preprocessing(configs=ensemble_configs, X_train=X_train, y_train=y_train, random_state=rng,
+                                cat_ix=cat_ix, n_workers=n_workers, parallel_mode="block")
+        configs, preprocessors, X_trains, y_trains, _ = list(zip(*itr))
+        model = model.to(device)
+        eng = model.engine(device)
+        prec = _precision(model, eng.device, autocast, force_inference_dtype)
+        costs = [float(len(y)) ** 2 for y in y_trains]
+        mine, gather = member_shard(len(configs), costs)
+        tokens = None
+        if image_train is not None and model.mixer_type in ("MGM", "MGM+CAP", "MoE") and mine:
+            tokens = eng.mixer_tokens(torch.from_numpy(np.asarray(image_train, np.float32)), prec)
+        caches = {}
+        for i in mine:
+            xt = None if X_trains[i] is None else torch.from_numpy(np.asarray(X_trains[i], np.float32))
+            caches[i] = eng.cache_build(xt, tokens, np.asarray(y_trains[i], np.float32), prec)
+        if mine:
+            eng.status()  # NaN in the encoded train rows (transformer.py:727-731,790-796)
+        return cls(save_peak_mem=save_peak_mem, dtype_byte_size=dtype_byte_size, caches=caches,
+                   ensemble_configs=configs, preprocessors=preprocessors, n_members=len(configs), model=model,
+                   precision=prec, mine=list(mine), gather=gather)
+
+    def iter_outputs(self, X, image_test, *, device: torch.device, autocast: bool) -> Iterator[tuple]:
+        eng = self.model.engine(self.model._device() if device.type != "cuda" else device)
+        tokens = None
+        if image_test is not None and self.model.mixer_type in ("MGM", "MGM+CAP", "MoE") and self.mine:
+            tokens = eng.mixer_tokens(torch.from_numpy(np.asarray(image_test, np.float32)), self.precision)
+        outs = {}
+        for i in self.mine:
+            xt = None
+            if X is not None and self.caches[i].F > 0:
+                xt = torch.from_numpy(np.asarray(self.preprocessors[i].transform(X).X, np.float32))
+            outs[i] = eng.cache_predict(self.caches[i], xt, tokens)
+        if self.mine:
+            eng.status()
+        Q = len(X) if X is not None else len(image_test)
+        for out, cfg in zip(self.gather(outs, eng.device, Q, self.model.cfg.n_out), self.ensemble_configs):
+            yield out, cfg
+

@@ -76,3 +76,24 @@ def test_low_memory_mode_is_reproducible(tmp_path):
     b = clf.predict_proba(d["X_test"], d["image_test"])
     np.testing.assert_array_equal(a, b)
     np.testing.assert_allclose(a.sum(1), 1.0, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_fit_with_cache_matches_reference(name, tmp_path):
+    """``fit_mode="fit_with_cache"``: train rows forwarded once at fit (train-KV cache on the
+    device), predict forwards the test rows only; same member logits as the reference's
+    fit_preprocessors goldens, twice in a row from one cache."""
+    case = _case(name)
+    z = np.load(HERE / "golden" / f"api_{name}.npz")
+    d = case_data(case)
+    clf = make_classifier(case, write_ckpt(case, tmp_path), inference_precision=torch.float32,
+                          fit_mode="fit_with_cache")
+    clf.fit(d["X_train"], d["image_train"], d["y_train"])
+    got = _spy(clf)
+    proba = clf.predict_proba(d["X_test"], d["image_test"])
+    for m, lg in enumerate(got):
+        ref = z[f"m{m}_logits"]
+        err = np.abs(lg - ref).max() / max(np.abs(ref).max(), 1e-6)
+        assert err < LOGIT_RTOL, (m, err)
+    np.testing.assert_allclose(proba, z["proba"], atol=PROBA_ATOL, rtol=0)
+    np.testing.assert_array_equal(clf.predict_proba(d["X_test"], d["image_test"]), proba)

@@ -331,3 +331,34 @@ def test_large_config_matches_oracle_on_device(name, S, N, F, n_cls, seed):
     assert (f32.argmax(1) == ref.argmax(1)).all()
     assert rel_err(b16, ref) <= BF16_TOL, (name, rel_err(b16, ref))
     assert (b16.argmax(1) == ref.argmax(1)).mean() >= 0.9
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+def test_train_kv_cache_equals_full_forward(prec):
+    """mmpfn_cache_build (train rows once) + mmpfn_cache_predict (test rows only) == the test
+    rows of one full forward, bitwise (every kernel computes a row independently of the others;
+    the encoders' statistics come from the train rows in both)."""
+    from synth import synth_image, synth_labels, synth_state_dict, synth_table
+
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    cfg = ModelConfig(nlayers=4, mgm_heads=8, cap_heads=4)
+    sd = synth_state_dict(state_dict_spec(cfg), 6)
+    model = make_model(cfg, sd)
+    eng = model.engine()
+    S, N, F = 520, 400, 11
+    x = torch.from_numpy(synth_table(S, F, 6, n_cat=4, nan_frac=0.02)).cuda()
+    im = torch.from_numpy(synth_image(S, 1, 6)).cuda()
+    y = synth_labels(S, 4, 6)[:N]
+    with torch.inference_mode():
+        tok = eng.mixer_tokens(im, prec)
+        full = eng.forward(x, tok, y, prec)
+        cache = eng.cache_build(x[:N], tok[:N], y, prec)
+        T = (F + 1) // 2 + tok.shape[1] + 1
+        assert cache.nbytes >= cfg.nlayers * 2 * T * 448 * 32 * (2 if prec else 4)  # head-0 K + V^T per layer
+        a = eng.cache_predict(cache, x[N:], tok[N:])
+        b = eng.cache_predict(cache, x[N:N + 37], tok[N:N + 37])  # any test batch size
+        eng.status()
+        cache.free()
+    assert torch.equal(a, full)
+    assert torch.equal(b, full[:37])
