@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--lanes", type=int, default=None, help="concurrent member lanes per GPU (default: engine's)")
     p.add_argument("--batch", type=int, default=None, help="members per batched forward (default: engine's)")
     p.add_argument("--api-steps", type=int, default=3, help="timed predict_proba calls of the API leg (0: skip)")
+    p.add_argument("--no-kv-cache", dest="kv_cache", action="store_false", help="skip the fit_with_cache leg")
     return p.parse_args()
 
 
@@ -181,6 +182,41 @@ def time_item_attention(eng, T, reps):
         "per_launch_ms": round(ms, 4),
         "per_launch_flop": flops,
     }
+
+
+def kv_cache_leg(eng, members, img, prec, steps):
+    """``fit_mode="fit_with_cache"`` serving rate: each member's train rows forwarded once
+    (cache build, timed separately), then every predict forwards only the Q test rows of each
+    member against its cached head-0 K/V (mmpfn_cache_predict).  Not the headline metric."""
+    N, Q = N_TRAIN, S_ROWS - N_TRAIN
+    tok = eng.mixer_tokens(img, prec)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    caches = [eng.cache_build(xm[:N], tok[:N], ym, prec) for xm, ym, _ in members]
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+
+    def predict():
+        tq = eng.mixer_tokens(img[N:], prec)
+        return eng.cache_predict_many(caches, [xm[N:] for xm, _, _ in members], tq)
+
+    predict()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        predict()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    out = {
+        "query_rows_per_s": round(len(members) * Q / dt, 1),
+        "ms_per_predict": round(dt * 1e3, 3),
+        "ms_cache_build_all_members": round(t_build * 1e3, 3),
+        "cache_bytes_per_member": caches[0].nbytes,
+        "note": "fit_with_cache: Q test rows per member against the device-resident train-KV cache",
+    }
+    for c in caches:
+        c.free()
+    return out
 
 
 def cpu_baseline(sd, x, y, image):
@@ -322,6 +358,7 @@ def main():
             api = api_end_to_end(cfg, sd, x, y, image, M, prec == _lib.PREC_F32, args.api_steps, world)
         except Exception as e:  # noqa: BLE001 - reported, the headline number stands on its own
             api = {"error": f"{type(e).__name__}: {e}"}
+    kv = kv_cache_leg(eng, [members[m] for m in mine], img, prec, args.steps) if args.kv_cache and mine else None
     roof = None
     if rank == 0:
         iso = time_item_attention(eng, T, args.attn_reps)
@@ -358,6 +395,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "api_end_to_end": api,
+            "kv_cache_predict": kv,
         }
         print(json.dumps(line))
     if world > 1:

@@ -229,6 +229,31 @@ class HipEngine:
         )
         return out
 
+    def cache_predict_many(self, caches, xs, tokens, lanes: int | None = None) -> list[torch.Tensor]:
+        """``cache_predict`` of several members, spread over concurrent lanes like ``forward_many``
+        (2 lanes: 4.5 ms vs 6.7 ms for 4 members' 460 test rows; 4 lanes measured no better)."""
+        n = len(caches)
+        lanes = max(1, min(int(self.lanes if lanes is None else lanes), n, _lib.MMPFN_MAX_LANES))
+        if lanes == 1:
+            return [self.cache_predict(c, x, tokens) for c, x in zip(caches, xs)]
+        main = torch.cuda.current_stream(self.device)
+        streams = self._lane_streams(lanes)
+        for st in streams:
+            st.wait_stream(main)
+        outs = []
+        try:
+            for k, (c, x) in enumerate(zip(caches, xs)):
+                with torch.cuda.stream(streams[k % lanes]):
+                    self._check(self.lib.mmpfn_select_lane(self.ctx, k % lanes), "mmpfn_select_lane")
+                    outs.append(self.cache_predict(c, x, tokens))
+        finally:
+            self._check(self.lib.mmpfn_select_lane(self.ctx, 0), "mmpfn_select_lane")
+            for st in streams:
+                main.wait_stream(st)
+        for o in outs:
+            o.record_stream(main)
+        return outs
+
     def forward_batch(self, items, precision: int) -> list[torch.Tensor]:
         """Members of ONE geometry (same S, N, F and tokens) in one batched forward
         (``mmpfn_forward_batch``: every layer kernel runs once over all members)."""

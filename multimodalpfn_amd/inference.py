@@ -219,12 +219,13 @@ class InferenceEngineCacheKV(InferenceEngine):
         tokens = None
         if image_test is not None and self.model.mixer_type in ("MGM", "MGM+CAP", "MoE") and self.mine:
             tokens = eng.mixer_tokens(torch.from_numpy(np.asarray(image_test, np.float32)), self.precision)
-        outs = {}
+        xts = []
         for i in self.mine:
             xt = None
             if X is not None and self.caches[i].F > 0:
                 xt = torch.from_numpy(np.asarray(self.preprocessors[i].transform(X).X, np.float32))
-            outs[i] = eng.cache_predict(self.caches[i], xt, tokens)
+            xts.append(xt)
+        outs = dict(zip(self.mine, eng.cache_predict_many([self.caches[i] for i in self.mine], xts, tokens)))
         if self.mine:
             eng.status()
         Q = len(X) if X is not None else len(image_test)
