@@ -10,8 +10,10 @@ namespace mmpfn {
 
 namespace {
 
-// one wave per row; two-pass mean / biased variance (torch layer_norm)
-template <typename TO>
+// one wave per row; two-pass mean / biased variance (torch layer_norm).  Rows with
+// dim % 4 == 0 and dim <= 4 * 64 * V4 are read once into registers as float4 (V4 per lane);
+// others take the strided three-pass loop.
+template <typename TO, int V4>
 __global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ in, int64_t rows, int dim, float eps,
                                                       TO* __restrict__ out, const float* __restrict__ g,
                                                       const float* __restrict__ b) {
@@ -19,20 +21,54 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ 
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const float* x = in + row * dim;
-  float s = 0.f;
-  for (int i = lane; i < dim; i += 64) s += x[i];
-  const float mean = wave_sum(s) / dim;
-  float q = 0.f;
-  for (int i = lane; i < dim; i += 64) {
-    const float d = x[i] - mean;
-    q += d * d;
-  }
-  const float inv = 1.0f / sqrtf(wave_sum(q) / dim + eps);
   TO* o = out + row * dim;
-  for (int i = lane; i < dim; i += 64) {
-    float v = (x[i] - mean) * inv;
-    if (g) v = v * g[i] + b[i];
-    o[i] = from_f32<TO>(v);
+  if constexpr (V4 > 0) {
+    const int n4 = dim >> 2;
+    f32x4 v[V4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < V4; ++j) {
+      const int i4 = lane + 64 * j;
+      v[j] = i4 < n4 ? *(const f32x4*)(x + 4 * i4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    }
+    const float mean = wave_sum(s) / dim;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < V4; ++j)
+      if (lane + 64 * j < n4)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[j][e] - mean;
+          q += d * d;
+        }
+    const float inv = 1.0f / sqrtf(wave_sum(q) / dim + eps);
+#pragma unroll
+    for (int j = 0; j < V4; ++j) {
+      const int i4 = lane + 64 * j;
+      if (i4 >= n4) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float w = (v[j][e] - mean) * inv;
+        if (g) w = w * g[4 * i4 + e] + b[4 * i4 + e];
+        o[4 * i4 + e] = from_f32<TO>(w);
+      }
+    }
+  } else {
+    float s = 0.f;
+    for (int i = lane; i < dim; i += 64) s += x[i];
+    const float mean = wave_sum(s) / dim;
+    float q = 0.f;
+    for (int i = lane; i < dim; i += 64) {
+      const float d = x[i] - mean;
+      q += d * d;
+    }
+    const float inv = 1.0f / sqrtf(wave_sum(q) / dim + eps);
+    for (int i = lane; i < dim; i += 64) {
+      float v = (x[i] - mean) * inv;
+      if (g) v = v * g[i] + b[i];
+      o[i] = from_f32<TO>(v);
+    }
   }
 }
 
@@ -177,10 +213,21 @@ hipError_t launch_layernorm_rows(const float* in, int64_t rows, int dim, float e
                                  const float* gamma, const float* beta, hipStream_t st) {
   if (rows <= 0) return hipSuccess;
   dim3 grid((rows + 3) / 4);
-  if (out_f32)
-    hipLaunchKernelGGL(ln_rows_kernel<float>, grid, dim3(256), 0, st, in, rows, dim, eps, (float*)out, gamma, beta);
-  else
-    hipLaunchKernelGGL(ln_rows_kernel<bf16>, grid, dim3(256), 0, st, in, rows, dim, eps, (bf16*)out, gamma, beta);
+  const int v4 = dim % 4 ? 0 : (dim / 4 + 63) / 64;  // float4 registers per lane
+  auto go = [&](auto tag, auto vc) {
+    using TO = decltype(tag);
+    hipLaunchKernelGGL((ln_rows_kernel<TO, decltype(vc)::value>), grid, dim3(256), 0, st, in, rows, dim, eps,
+                       (TO*)out, gamma, beta);
+  };
+  auto pick = [&](auto tag) {
+    if (v4 == 1) go(tag, std::integral_constant<int, 1>{});
+    else if (v4 == 2) go(tag, std::integral_constant<int, 2>{});
+    else if (v4 == 3) go(tag, std::integral_constant<int, 3>{});
+    else if (v4 == 4) go(tag, std::integral_constant<int, 4>{});
+    else go(tag, std::integral_constant<int, 0>{});
+  };
+  if (out_f32) pick(float{});
+  else pick(bf16{});
   return hipGetLastError();
 }
 
