@@ -46,8 +46,8 @@ MGM, CAP, MEMBERS_PER_GPU = 64, 24, 4
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
     p.add_argument("--members", type=int, default=MEMBERS_PER_GPU, help="members per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
