@@ -184,6 +184,25 @@ def time_item_attention(eng, T, reps):
     }
 
 
+def forward_flops(T, S=S_ROWS, N=N_TRAIN, E=192, FF=768, L=12) -> float:
+    """Algorithmic flops of one member forward's layer stack:
+    feature attention (QKV, T x T attention, out-projection), item attention (Q of all rows,
+    K/V of the train rows, train + test-MQA attention, out-projection) and the MLP."""
+    Q = S - N
+    feat = 2 * S * T * E * 3 * E + 4 * S * T * T * E + 2 * S * T * E * E
+    item = 2 * S * T * E * E + 2 * N * T * E * 2 * E + 4 * T * N * N * E + 4 * T * Q * N * E + 2 * S * T * E * E
+    mlp = 4 * S * T * E * FF
+    return float(L * (feat + item + mlp))
+
+
+def mixer_flops(S=S_ROWS, D=768, E=192, mgm=MGM, cap=CAP) -> float:
+    """MGM (per head Linear(768,768) + Linear(384,192)) and CAP (K|V projection of the
+    mgm tokens, attention, out-projection, FFN) of one predict (A7-A8)."""
+    mg = 2 * S * mgm * (D * D + (D // 2) * E)
+    cp = 2 * S * mgm * E * 2 * E + 4 * S * cap * mgm * E + 2 * S * cap * (E * E + E * 2 * E + 2 * E * E)
+    return float(mg + cp)
+
+
 def kv_cache_leg(eng, members, img, prec, steps):
     """``fit_mode="fit_with_cache"`` serving rate: each member's train rows forwarded once
     (cache build, timed separately), then every predict forwards only the Q test rows of each
@@ -351,6 +370,8 @@ def main():
         dt = float(tt.item())
     rows = M * S_ROWS * args.steps
     value = rows / dt
+    step_flop = len(mine) * forward_flops(T) + mixer_flops()  # per rank
+    wf = step_flop * args.steps / dt / 1e12  # TFLOP/s of one rank (its wall time is the job's max)
 
     api = None
     if args.api_steps > 0:
@@ -393,6 +414,13 @@ def main():
                 "parallelism": f"ensemble members sharded over {world} GPU(s) + RCCL all-gather of logits",
             },
             "roofline": roof,
+            "whole_forward": {
+                "tflop_per_step_per_gpu": round(step_flop / 1e12, 3),
+                "achieved": round(wf, 1),
+                "unit": "TFLOP/s per GPU",
+                "frac": round(wf / BF16_PEAK_TFLOPS, 4),
+                "note": "algorithmic flops of the mixer + every member's 12-layer stack (SURVEY.md 8d) / step time",
+            },
             "cpu_baseline": cpu,
             "api_end_to_end": api,
             "kv_cache_predict": kv,
