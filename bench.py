@@ -385,6 +385,9 @@ def main():
         iso = time_item_attention(eng, T, args.attn_reps)
         roof = live if live is not None else iso
         roof["isolated_single_member_launch"] = {k: iso[k] for k in ("achieved", "frac", "per_launch_ms", "traffic")}
+        if live is not None and live["token_columns_per_launch"] != T:  # the step's launch shape, alone
+            isb = time_item_attention(eng, live["token_columns_per_launch"], args.attn_reps)
+            roof["isolated_same_shape_launch"] = {k: isb[k] for k in ("achieved", "frac", "per_launch_ms", "traffic")}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sd, x, y, image)
