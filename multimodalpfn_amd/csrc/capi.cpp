@@ -187,6 +187,18 @@ std::vector<float> pack_mlp2_perm(const std::vector<float>& w, int E, int Fh) {
   return o;
 }
 
+// W1 [Fh][E] with the K (feature) order of mlp_rows_kernel's X fragments: K position
+// 32ks + 8g + j holds feature 32ks + 16(j/4) + 4g + (j%4) (the Y^T lane layout, E = 192)
+std::vector<float> pack_mlp1_perm(const std::vector<float>& w, int E, int Fh) {
+  std::vector<float> o(w.size());
+  for (int h = 0; h < Fh; ++h)
+    for (int k = 0; k < E; ++k) {
+      const int ks = k / 32, g = (k % 32) / 8, j = k % 8;
+      o[(size_t)h * E + k] = w[(size_t)h * E + 32 * ks + 16 * (j / 4) + 4 * g + (j % 4)];
+    }
+  return o;
+}
+
 // featrow.hip weight pack (FEAT_PACK_LAYER floats, LDS images with FEAT_IMG_STRIDE-wide rows,
 // the 16 pad columns zero):
 //   per head h, rows [0,32) : Wq row 8(rho>>2) + 4f + (rho&3) for image row 16f + rho, scaled by
@@ -257,7 +269,8 @@ int finalize(mmpfn_ctx* ctx) {
       if ((rc = upload(ctx, L.feat_pack_h, pack_feat_rows(*fq, transpose_out(*fo, HD, E), d.nhead, E), true)))
         return rc;
     if ((rc = up2(ctx, L.item_out, L.item_out_h, transpose_out(*io, HD, E)))) return rc;
-    if ((rc = up2(ctx, L.mlp1, L.mlp1_h, *m1))) return rc;
+    if ((rc = upload(ctx, L.mlp1, *m1, false))) return rc;
+    if ((rc = upload(ctx, L.mlp1_h, E == 192 ? pack_mlp1_perm(*m1, E, Fh) : *m1, true))) return rc;
     if ((rc = upload(ctx, L.mlp2, *m2, false))) return rc;
     if ((rc = upload(ctx, L.mlp2_h, pack_mlp2_perm(*m2, E, Fh), true))) return rc;
     std::vector<float> wtrain((size_t)3 * HD * E), wtest((size_t)HD * E);
@@ -651,7 +664,9 @@ int run_layer(mmpfn_ctx* ctx, int l) {
       if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, N, Q, N, 0, prec, st));
     }
     }
-    if (bf && E == 192) {
+    if (bf && E == 192 && d.nhid % 32 == 0) {
+      // the out-projection + residual + LN runs as the prologue of the MLP kernel below
+    } else if (bf && E == 192) {
       HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, RM, Xall, d.ln_eps, st));
     } else {
       GemmArgs b = gargs();
@@ -661,8 +676,9 @@ int run_layer(mmpfn_ctx* ctx, int l) {
     }
   }
   // ---- MLP (mlp.py:93-104), fused up/GELU/down/residual/LN, all members' tokens
-  if (bf && d.nhid % 32 == 0)  // W2 bf16 copy is stored in mlp_rows_kernel's permuted K order
-    HIPCHK(launch_mlp_rows(Xall, L.mlp1_h.p, L.mlp2_h.p, RM, E, d.nhid, d.ln_eps, st));
+  if (bf && E == 192 && d.nhid % 32 == 0)  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders; fused out-proj
+    HIPCHK(launch_mlp_rows(Xall, L.mlp1_h.p, L.mlp2_h.p, RM, E, d.nhid, d.ln_eps, st, ctx->ws_O.p,
+                           L.item_out_h.p));
   else
     HIPCHK(launch_mlp_fused(Xall, L.mlp1.p, L.mlp2.p, RM, E, d.nhid, d.ln_eps, PREC_F32, st));
   return MMPFN_OK;

@@ -56,8 +56,10 @@ hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M,
 
 // row-resident MLP sublayer (bf16 only, mlp_rows.hip): W1 [Fh][E] bf16, W2 [E][Fh] bf16 in the
 // permuted hidden order of pack_mlp2_perm (capi.cpp); Fh % 32 == 0, E == 192
-hipError_t launch_mlp_rows(float* X, const void* W1, const void* W2perm, int64_t M, int E, int Fh, float eps,
-                           hipStream_t st);
+// W1perm: W1 with its K (feature) order permuted to the Y^T lane layout (capi.cpp pack_mlp1_perm);
+// O / Wout non-null: X <- LN(X + O Wout^T) first (the item-attention out-projection, fused)
+hipError_t launch_mlp_rows(float* X, const void* W1perm, const void* W2perm, int64_t M, int E, int Fh, float eps,
+                           hipStream_t st, const void* O = nullptr, const void* Wout = nullptr);
 
 // row-resident item-attention projections (bf16, K = 192, rowgemm.hip):
 //   QKV: X rows (remap (m/rdiv)*rmul + (m%rdiv)*rmul2 + roff) . W^T, W [N][192] (N = 576 or 192),

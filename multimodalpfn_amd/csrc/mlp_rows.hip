@@ -1,8 +1,12 @@
 // Row-resident MLP sublayer for gfx950 (bf16 performance mode):
 //   X <- LayerNorm(X + GELU(X W1^T) W2^T)           (mlp.py:93-104, layer.py:437-455)
+// optionally fused with the item-attention out-projection before it (RES):
+//   X <- LayerNorm(X + O Wout^T) first              (layer.py:341-379,437-455)
 //
 // Each wave owns 32 rows (tokens) for the whole sublayer and keeps them in registers:
-//   * its rows of X, as bf16 B-operand fragments (A^T), loaded once from HBM;
+//   * its rows of X, as bf16 B-operand fragments (A^T), loaded once from HBM -- in the lane
+//     layout of a Y^T accumulator (lane = row, features 16f + 4g + i), W1's K order permuted
+//     to match (capi.cpp pack_mlp1_perm), so RES can feed its LayerNorm output straight in;
 //   * the hidden activations of a 32-wide hidden chunk, computed transposed
 //     (H^T = W1c . A^T) so the accumulator of one 16x16 tile pair is, lane for lane, the B
 //     operand of the down projection (Y^T += W2c . H^T) once the chunk's K order is
@@ -37,14 +41,16 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // TT = 16-row tiles per wave: 2 (32 rows, two waves per SIMD, accumulators in VGPRs) or 4 (64 rows,
 // one wave per SIMD with the 192 x 64 Y^T accumulator in AGPRs -- half the LDS weight reads per row,
 // but measured 15% slower: one wave cannot hide the LDS / GELU latency the second wave covers)
-template <int TT>
+template <int TT, bool RES>
 __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* __restrict__ X,
                                                                        const bf16* __restrict__ W1,
                                                                        const bf16* __restrict__ W2p, int M, int Fh,
-                                                                       float eps) {
+                                                                       float eps, const bf16* __restrict__ O,
+                                                                       const bf16* __restrict__ Wout) {
   constexpr int RROWS = 4 * 16 * TT;  // rows per block
-  __shared__ __attribute__((aligned(16))) bf16 w1s[2 * W1EL];
-  __shared__ __attribute__((aligned(16))) bf16 w2s[2 * W2EL];
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * W1EL + 2 * W2EL];
+  bf16* const w1s = lds;
+  bf16* const w2s = lds + 2 * W1EL;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * RROWS + wave * 16 * TT;
@@ -82,22 +88,107 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
     }
   };
 
-  fetch1(0);
-  fetch2(0);
-  // the wave's rows as A^T fragments: lane = row (tile tt, col fr), 8 consecutive features
+  // ---- the wave's rows as B fragments in the Y^T lane layout: lane (row 16tt + fr, group fg)
+  //      holds features 16f + 4fg + i; K position 32ks + 8fg + j <-> feature of tile f = 2ks + j/4
   bf16x8 af[TT][RE / 32];
-#pragma unroll
-  for (int tt = 0; tt < TT; ++tt) {
-    const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
-    const float* xr = X + m * RE + fg * 8;
+  f32x4 y[RE / 16][TT];
+  auto to_af = [&](int tt) {
 #pragma unroll
     for (int ks = 0; ks < RE / 32; ++ks) {
-      const f32x4 lo = *(const f32x4*)(xr + ks * 32);
-      const f32x4 hi = *(const f32x4*)(xr + ks * 32 + 4);
       bf16x8 b;
-      b[0] = (bf16)lo[0], b[1] = (bf16)lo[1], b[2] = (bf16)lo[2], b[3] = (bf16)lo[3];
-      b[4] = (bf16)hi[0], b[5] = (bf16)hi[1], b[6] = (bf16)hi[2], b[7] = (bf16)hi[3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[i] = (bf16)y[2 * ks][tt][i], b[4 + i] = (bf16)y[2 * ks + 1][tt][i];
       af[tt][ks] = b;
+    }
+  };
+  if constexpr (RES) {
+    // X <- LayerNorm(X + O . Wout^T): Wout [192 out][192 in] staged in two 96-row halves through
+    // the (still unused) weight slots, C^T tiles (lane = row) as in rowgemm_resln
+    bf16x8 ao[TT][RE / 32];
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
+#pragma unroll
+      for (int ks = 0; ks < RE / 32; ++ks) ao[tt][ks] = *(const bf16x8*)(O + m * RE + ks * 32 + fg * 8);
+    }
+#pragma unroll
+    for (int f = 0; f < RE / 16; ++f)
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt) y[f][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      constexpr int PC = 96 * (RE / 8) / 256;  // 16-B pieces per thread (9)
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {            // three rounds of 3 pieces: bounded staging registers
+        u32x4 st[PC / 3];
+#pragma unroll
+        for (int j = 0; j < PC / 3; ++j) {
+          const int pc = tid + 256 * (r * (PC / 3) + j);
+          st[j] = *(const u32x4*)(Wout + (int64_t)(96 * half + pc / 24) * RE + (pc % 24) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < PC / 3; ++j) {
+          const int pc = tid + 256 * (r * (PC / 3) + j);
+          *(u32x4*)(lds + (pc / 24) * W1ST + (pc % 24) * 8) = st[j];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ks = 0; ks < RE / 32; ++ks)
+#pragma unroll
+        for (int fl = 0; fl < 6; ++fl) {
+          const bf16x8 w = *(const bf16x8*)(lds + (fl * 16 + fr) * W1ST + ks * 32 + fg * 8);
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) y[6 * half + fl][tt] = mfma16(w, ao[tt][ks], y[6 * half + fl][tt]);
+        }
+      __syncthreads();
+    }
+    // residual + LayerNorm (layer.py:437-455), X' written back (the MLP's residual) and packed
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      const int64_t m = m0 + tt * 16 + fr;
+      const bool valid = m < M;
+      float* xr = X + (valid ? m : (int64_t)M - 1) * RE + fg * 4;
+      float sm = 0.f;
+#pragma unroll
+      for (int f = 0; f < RE / 16; ++f) {
+        const f32x4 xv = *(const f32x4*)(xr + f * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          y[f][tt][i] += xv[i];
+          sm += y[f][tt][i];
+        }
+      }
+      const float mean = sum_rows4(sm) * (1.0f / RE);
+      float q = 0.f;
+#pragma unroll
+      for (int f = 0; f < RE / 16; ++f)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float dl = y[f][tt][i] - mean;
+          q += dl * dl;
+        }
+      const float inv = 1.0f / sqrtf(sum_rows4(q) * (1.0f / RE) + eps);
+#pragma unroll
+      for (int f = 0; f < RE / 16; ++f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[f][tt][i] = (y[f][tt][i] - mean) * inv;
+        if (valid) *(f32x4*)(xr + f * 16) = y[f][tt];
+      }
+      to_af(tt);
+    }
+    fetch1(0);
+    fetch2(0);
+  } else {
+    fetch1(0);
+    fetch2(0);
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
+      const float* xr = X + m * RE + fg * 4;
+#pragma unroll
+      for (int f = 0; f < RE / 16; ++f) y[f][tt] = *(const f32x4*)(xr + f * 16);
+      to_af(tt);
     }
   }
   stash1(0);
@@ -133,7 +224,6 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
           wa[ks % PU][ht] = *(const bf16x8*)(w1 + (ht * 16 + fr) * W1ST + (ks + PU) * 32 + fg * 8);
     }
   };
-  f32x4 y[RE / 16][TT];
 #pragma unroll
   for (int o = 0; o < RE / 16; ++o)
 #pragma unroll
@@ -234,16 +324,21 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
 
 }  // namespace
 
-hipError_t launch_mlp_rows(float* X, const void* W1, const void* W2perm, int64_t M, int E, int Fh, float eps,
-                           hipStream_t st) {
+hipError_t launch_mlp_rows(float* X, const void* W1perm, const void* W2perm, int64_t M, int E, int Fh, float eps,
+                           hipStream_t st, const void* O, const void* Wout) {
   if (M <= 0) return hipSuccess;
   if (E != RE || Fh % RHC != 0) return hipErrorInvalidValue;
 #ifndef MLP_TT
 #define MLP_TT 2  // 4 measured slower: 202 vs 175 us per two-member launch
 #endif
   constexpr int RROWS = 64 * MLP_TT;
-  hipLaunchKernelGGL(mlp_rows_kernel<MLP_TT>, dim3((unsigned)((M + RROWS - 1) / RROWS)), dim3(256), 0, st, X,
-                     (const bf16*)W1, (const bf16*)W2perm, (int)M, Fh, eps);
+  const dim3 grid((unsigned)((M + RROWS - 1) / RROWS)), block(256);
+  if (O)
+    hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, true>), grid, block, 0, st, X, (const bf16*)W1perm,
+                       (const bf16*)W2perm, (int)M, Fh, eps, (const bf16*)O, (const bf16*)Wout);
+  else
+    hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, false>), grid, block, 0, st, X, (const bf16*)W1perm,
+                       (const bf16*)W2perm, (int)M, Fh, eps, nullptr, nullptr);
   return hipGetLastError();
 }
 
