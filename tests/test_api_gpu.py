@@ -97,3 +97,46 @@ def test_fit_with_cache_matches_reference(name, tmp_path):
         assert err < LOGIT_RTOL, (m, err)
     np.testing.assert_allclose(proba, z["proba"], atol=PROBA_ATOL, rtol=0)
     np.testing.assert_array_equal(clf.predict_proba(d["X_test"], d["image_test"]), proba)
+
+
+_FIT_MATRIX = [(fs, cs, fm, ip, ro)
+               for fs in ("shuffle", "rotate")
+               for cs in ("shuffle", "rotate")
+               for fm in ("low_memory", "fit_preprocessors", "fit_with_cache")
+               for ip in ("auto", "autocast", torch.float64)
+               for ro in (None, 12)]
+
+
+@pytest.fixture(scope="module")
+def iris_ckpt(tmp_path_factory):
+    return write_ckpt(_case("tab_default"), tmp_path_factory.mktemp("iris"))
+
+
+@pytest.mark.parametrize("feature_shift,class_shift,fit_mode,precision,outlier_std", _FIT_MATRIX)
+def test_fit_matrix(feature_shift, class_shift, fit_mode, precision, outlier_std, iris_ckpt):
+    """The reference's ``tests/test_classifier_interface.py:47-94`` matrix (shift decoders x
+    fit modes x inference precision x outlier removal) on iris, tabular only: ``fit`` returns
+    the estimator, it is fitted, probabilities are ``[n, n_classes]`` rows summing to 1 and
+    ``predict`` is ``[n]`` of the train labels."""
+    import sklearn.datasets
+    from sklearn.utils.validation import check_is_fitted
+
+    from multimodalpfn_amd import MMPFNClassifier
+
+    X, y = sklearn.datasets.load_iris(return_X_y=True)
+    clf = MMPFNClassifier(model_path=str(iris_ckpt), device="cuda", fit_mode=fit_mode,
+                          inference_precision=precision, mixer_type="MGM+CAP", mgm_heads=2, cap_heads=2,
+                          features_per_group=2,
+                          inference_config={"OUTLIER_REMOVAL_STD": outlier_std,
+                                            "CLASS_SHIFT_METHOD": class_shift,
+                                            "FEATURE_SHIFT_METHOD": feature_shift})
+    assert clf.fit(X, None, y) is clf
+    check_is_fitted(clf)
+    assert clf.use_autocast_ == (precision != torch.float64)
+    proba = clf.predict_proba(X, None)
+    assert proba.shape == (X.shape[0], len(np.unique(y)))
+    assert np.isfinite(proba).all()
+    np.testing.assert_allclose(proba.sum(1), 1.0, atol=1e-5)
+    pred = clf.predict(X, None)
+    assert pred.shape == (X.shape[0],)
+    assert set(np.unique(pred)) <= set(np.unique(y))
