@@ -553,8 +553,14 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
       for (int qb = 0; qb < A2_NCH; ++qb)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
+#if defined(A2_PRIO) && A2_PRIO > 1
+          __builtin_amdgcn_s_setprio(1);
+#endif
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qf[qb][0], negm[qb], 0, 0, 0);
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][1], qf[qb][1], s[qb][u], 0, 0, 0);
+#if defined(A2_PRIO) && A2_PRIO > 1
+          __builtin_amdgcn_s_setprio(0);
+#endif
         }
       if constexpr (MASK) {
 #pragma unroll
@@ -594,9 +600,15 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 #else
             for (int j = 0; j < 8; ++j) pb[j] = (bf16)s[qb][u][8 * sp + j];
 #endif
+#ifdef A2_PRIO
+            __builtin_amdgcn_s_setprio(1);
+#endif
             o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[u][sp], pb, o[qb], 0, 0, 0);
 #ifndef A2_NOSEL
             lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[qb], 0, 0, 0);
+#endif
+#ifdef A2_PRIO
+            __builtin_amdgcn_s_setprio(0);
 #endif
           }
     }

@@ -155,11 +155,24 @@ __device__ __forceinline__ void chunk_mma(const bf16* W, const bf16x8 (&af)[2][G
   }
 }
 
-__global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p) {
-  __shared__ __attribute__((aligned(16))) bf16 Ws[2 * QCEL];
+// Per-wave output staging: the chunk's C tile goes through LDS so that every global store
+// writes 16 B per lane in contiguous runs -- Q / K: [32 rows][64 features] (2 KB per head
+// and wave, whole 1 KB per instruction), V^T: [64 features][32 rows] (64-B runs of 32 keys).
+// Blocks never straddle a column b (grid = column x row tiles), so a wave's 32 rows are
+// consecutive positions starting at a multiple of 32 (+ a_roff).
+constexpr int OQST = QC + 8;    // Q/K tile row stride (bf16): 144 B
+constexpr int OVST = 32 + 8;    // V^T tile row stride (bf16): 80 B
+constexpr int OWEL = QC * OVST; // per-wave staging elements (>= 32 * OQST)
+static_assert(32 * OQST <= OWEL, "Q/K staging tile must fit");
+
+__global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p, int tiles_per_b) {
+  __shared__ __attribute__((aligned(16))) bf16 Ws[2 * QCEL + 4 * OWEL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const int64_t m0 = (int64_t)blockIdx.x * GROWS + wave * 32;
+  const int rd = (int)p.a_rdiv;
+  const int b = blockIdx.x / tiles_per_b;
+  const int l0 = (blockIdx.x - b * tiles_per_b) * GROWS + wave * 32;  // wave's first row inside column b
+  bf16* const Os = Ws + 2 * QCEL + wave * OWEL;
   const int nch = p.N / QC;
   u32x4 r[QCP];
   auto fetch = [&](int c) {
@@ -178,69 +191,97 @@ __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p) {
   };
   fetch(0);
   bf16x8 af[2][GE / 32];
-  load_rows<true>(p, m0, fr, fg, af);
+  {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int l = min(l0 + tt * 16 + fr, rd - 1);
+      const float* xr = (const float*)p.A + ((int64_t)b * p.a_rmul + (int64_t)l * p.a_rmul2 + p.a_roff) * GE + fg * 8;
+      f32x4 lo[GE / 32], hi[GE / 32];
+#pragma unroll
+      for (int ks = 0; ks < GE / 32; ++ks) {
+        lo[ks] = *(const f32x4*)(xr + ks * 32);
+        hi[ks] = *(const f32x4*)(xr + ks * 32 + 4);
+      }
+#pragma unroll
+      for (int ks = 0; ks < GE / 32; ++ks) {
+        bf16x8 v;
+        v[0] = (bf16)lo[ks][0], v[1] = (bf16)lo[ks][1], v[2] = (bf16)lo[ks][2], v[3] = (bf16)lo[ks][3];
+        v[4] = (bf16)hi[ks][0], v[5] = (bf16)hi[ks][1], v[6] = (bf16)hi[ks][2], v[7] = (bf16)hi[ks][3];
+        af[tt][ks] = v;
+      }
+    }
+  }
   stash(0);
   if (nch > 1) fetch(1);
   __syncthreads();
-  int rd = (int)p.a_rdiv;
+  const int pos0 = (int)p.a_roff + l0;  // attention position of the wave's row 0
   for (int c = 0; c < nch; ++c) {
+#ifndef RG_NOSTAGE
     if (c + 1 < nch) stash((c + 1) & 1);
     if (c + 2 < nch) fetch(c + 2);
     const bf16* W = Ws + (c & 1) * QCEL;
+#else
+    const bf16* W = Ws;
+#endif
     const int n0 = c * QC, j = n0 / GE;  // 0 q, 1 k, 2 v
+    const int h0 = (n0 - j * GE) >> 5;   // first of the chunk's two heads
     f32x4 acc[QC / 16][2];
 #pragma unroll
     for (int f = 0; f < QC / 16; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (j < 2) {
       chunk_mma<true>(W, af, fr, fg, acc);
-      // C^T: lane = row m (tile tt, col fr); rows of the tile = features n0 + 16f + 4fg + i
+      // C^T: lane = row 16tt + fr, features 16f + 4fg + i  ->  Os[row][feature]
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const int m = (int)(m0 + tt * 16 + fr);
-        if (m >= p.M) continue;
-        const int b = m / rd, pos = (int)p.a_roff + (m - b * rd);
-        bf16* base = j == 0 ? p.q + ((int64_t)b * p.H * p.S + pos) * 32 : p.k + ((int64_t)b * p.H * p.Npad + pos) * 32;
-        const int64_t hstride = (int64_t)(j == 0 ? p.S : p.Npad) * 32;
+      for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int f = 0; f < QC / 16; ++f) {
-          const int n = (n0 - j * GE) + f * 16 + fg * 4;  // 4 consecutive features of one head
           bf16x4 o;
           o[0] = (bf16)acc[f][tt][0], o[1] = (bf16)acc[f][tt][1];
           o[2] = (bf16)acc[f][tt][2], o[3] = (bf16)acc[f][tt][3];
-          *(bf16x4*)(base + (n >> 5) * hstride + (n & 31)) = o;
+          *(bf16x4*)(Os + (tt * 16 + fr) * OQST + f * 16 + fg * 4) = o;
         }
-      }
+      bf16* base = j == 0 ? p.q + (((int64_t)b * p.H + h0) * p.S + pos0) * 32
+                          : p.k + (((int64_t)b * p.H + h0) * p.Npad + pos0) * 32;
+      const int64_t hstride = (int64_t)(j == 0 ? p.S : p.Npad) * 32;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = 16 * i + (lane >> 2), cc = lane & 3;
+          const u32x4 v = *(const u32x4*)(Os + row * OQST + hh * 32 + cc * 8);
+          if (l0 + row < rd) *(u32x4*)(base + hh * hstride + row * 32 + cc * 8) = v;
+        }
     } else {
       chunk_mma<false>(W, af, fr, fg, acc);
-      // C: lane = feature n (tile f, col fr); rows of the tile = rows m0 + 16tt + 4fg + i
+      // C: lane = feature 16f + fr, rows 16tt + 4fg + i  ->  Os[feature][row]
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const int ma = (int)(m0 + tt * 16 + fg * 4);
-        if (ma >= p.M) continue;
-        const int b = ma / rd, pos = (int)p.a_roff + (ma - b * rd);
-        const bool whole = ma + 3 < p.M && (ma - b * rd) + 3 < rd && (pos & 3) == 0;
+      for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int f = 0; f < QC / 16; ++f) {
-          const int n = (n0 - 2 * GE) + f * 16 + fr;
-          if (whole) {
-            bf16x4 o;
-            o[0] = (bf16)acc[f][tt][0], o[1] = (bf16)acc[f][tt][1];
-            o[2] = (bf16)acc[f][tt][2], o[3] = (bf16)acc[f][tt][3];
-            *(bf16x4*)(p.vt + ((int64_t)(b * p.H + (n >> 5)) * 32 + (n & 31)) * p.Npad + pos) = o;
-          } else {
+          bf16x4 o;
+          o[0] = (bf16)acc[f][tt][0], o[1] = (bf16)acc[f][tt][1];
+          o[2] = (bf16)acc[f][tt][2], o[3] = (bf16)acc[f][tt][3];
+          *(bf16x4*)(Os + (f * 16 + fr) * OVST + tt * 16 + fg * 4) = o;
+        }
+      bf16* base = p.vt + ((int64_t)b * p.H + h0) * 32 * p.Npad + pos0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {  // fully unrolled: a runtime index would put acc in scratch
-              const int m = ma + i;
-              if (m < p.M) {
-                const int bi = m / rd, pi = (int)p.a_roff + (m - bi * rd);
-                p.vt[((int64_t)(bi * p.H + (n >> 5)) * 32 + (n & 31)) * p.Npad + pi] = (bf16)acc[f][tt][i];
-              }
-            }
-          }
+      for (int i = 0; i < 4; ++i) {
+        const int feat = 16 * i + (lane >> 2), rr = (lane & 3) * 8;
+        const u32x4 v = *(const u32x4*)(Os + feat * OVST + rr);
+        bf16* dst = base + (int64_t)feat * p.Npad + rr;  // feature = (head - h0) * 32 + d
+        if (l0 + rr + 8 <= rd) {
+          *(u32x4*)dst = v;
+        } else {
+          const bf16x8 e = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (l0 + rr + k < rd) dst[k] = e[k];
         }
       }
     }
+#ifndef RG_NOSYNC
     __syncthreads();
+#endif
   }
 }
 
@@ -306,7 +347,12 @@ hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, in
   a.A = X, a.a_rdiv = a_rdiv, a.a_rmul = a_rmul, a.a_rmul2 = a_rmul2, a.a_roff = a_roff;
   a.W = (const bf16*)W, a.M = M, a.N = N;
   a.q = (bf16*)q, a.k = (bf16*)k, a.vt = (bf16*)vt, a.S = S, a.Npad = Npad, a.H = H;
-  hipLaunchKernelGGL(rowgemm_qkv2_kernel, dim3((M + GROWS - 1) / GROWS), dim3(256), 0, st, a);
+  // blocks tile each column b separately: nb = M / a_rdiv columns of a_rdiv rows
+  if (a_rdiv <= 0 || M % a_rdiv != 0) return hipErrorInvalidValue;
+  if (N == 3 * GE && (a_roff % 8 != 0 || a_roff + a_rdiv > Npad)) return hipErrorInvalidValue;  // 16-B V^T stores
+  const int tiles = (int)((a_rdiv + GROWS - 1) / GROWS);
+  const int64_t nblk = (int64_t)tiles * (M / a_rdiv);
+  hipLaunchKernelGGL(rowgemm_qkv2_kernel, dim3((unsigned)nblk), dim3(256), 0, st, a, tiles);
   return hipGetLastError();
 }
 
