@@ -11,7 +11,8 @@
 //     (H^T = W1c . A^T) so the accumulator of one 16x16 tile pair is, lane for lane, the B
 //     operand of the down projection (Y^T += W2c . H^T) once the chunk's K order is
 //     permuted (pos 8g+j <-> hidden 4g+j / 16+4g+j-4; W2 stored so, capi.cpp pack_mlp2_perm);
-//   * the 192 x 32 output accumulator Y^T, then residual + LayerNorm across lanes.
+//   * the 192 x 32 output accumulator Y^T, initialised with the fp32 residual itself (X, or the
+//     fused prologue's X'), so the residual never leaves registers; then LayerNorm across lanes.
 // Software pipeline over hidden chunks c (branch-free body, last chunk peeled): GELU(H(c)) on
 // the VALU beside the MFMAs of H(c+1), then Y^T += W2c . GELU(H(c)); one barrier per chunk.
 // Only the weights move through LDS: a 128-row block (4 waves) shares each chunk; W1 of chunk
@@ -170,11 +171,9 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
         }
       const float inv = 1.0f / sqrtf(sum_rows4(q) * (1.0f / RE) + eps);
 #pragma unroll
-      for (int f = 0; f < RE / 16; ++f) {
+      for (int f = 0; f < RE / 16; ++f)
 #pragma unroll
         for (int i = 0; i < 4; ++i) y[f][tt][i] = (y[f][tt][i] - mean) * inv;
-        if (valid) *(f32x4*)(xr + f * 16) = y[f][tt];
-      }
       to_af(tt);
     }
     fetch1(0);
@@ -224,10 +223,8 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
           wa[ks % PU][ht] = *(const bf16x8*)(w1 + (ht * 16 + fr) * W1ST + (ks + PU) * 32 + fg * 8);
     }
   };
-#pragma unroll
-  for (int o = 0; o < RE / 16; ++o)
-#pragma unroll
-    for (int tt = 0; tt < TT; ++tt) y[o][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // y holds the residual (X, or X' after the fused prologue) in fp32: the down-projection MFMAs
+  // accumulate onto it, so the residual is never written out and read back
   f32x4 h[2][TT];
   hmma(w1s, h);
 
@@ -290,14 +287,9 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
     float* xr = X + (valid ? m : (int64_t)M - 1) * RE + fg * 4;
     float s = 0.f;
 #pragma unroll
-    for (int o = 0; o < RE / 16; ++o) {
-      const f32x4 xv = *(const f32x4*)(xr + o * 16);
+    for (int o = 0; o < RE / 16; ++o)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        y[o][tt][i] += xv[i];
-        s += y[o][tt][i];
-      }
-    }
+      for (int i = 0; i < 4; ++i) s += y[o][tt][i];
     s = sum_rows4(s);
     const float mean = s * (1.0f / RE);
     float q = 0.f;
@@ -316,7 +308,11 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
         f32x4 ov;
 #pragma unroll
         for (int i = 0; i < 4; ++i) ov[i] = (y[o][tt][i] - mean) * inv;
+#ifndef MLP_NOSTORE
         *(f32x4*)(xr + o * 16) = ov;
+#else
+        if (ov[0] == 1234.5f && ov[3] == 4321.f) xr[o] = ov[1];
+#endif
       }
     }
   }
