@@ -714,7 +714,10 @@ int mixer(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, i
     GemmArgs a = gargs();
     a.A = ctx->mx[0].p, a.lda = D, a.W = W(ctx->mgm_w1, ctx->mgm_w1_h, prec), a.bias = (const float*)ctx->mgm_b1.p;
     a.M = (int)rows, a.N = mg * D, a.K = D, a.C = ctx->mx[1].p, a.ldc = (int64_t)mg * (D / 2);
-    HIPCHK(launch_gemm(a, prec, EPI_GLU, !bf, !bf, 1, st));
+    if (bf && (mg * D) % 256 == 0 && D % 64 == 0)
+      HIPCHK(launch_gemm_glu_big(ctx->mx[0].p, a.W, a.bias, ctx->mx[1].p, (int)rows, mg * D, D, st));
+    else
+      HIPCHK(launch_gemm(a, prec, EPI_GLU, !bf, !bf, 1, st));
     GemmArgs b = gargs();
     b.A = ctx->mx[1].p, b.lda = (int64_t)mg * (D / 2), b.a_zstride = D / 2;
     b.W = W(ctx->mgm_w2, ctx->mgm_w2_h, prec), b.w_zstride = (int64_t)E * (D / 2);

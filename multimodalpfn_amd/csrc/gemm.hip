@@ -349,6 +349,121 @@ hipError_t launch_e(const GemmArgs& a, int epi, int groups, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------- large-tile GLU GEMM (bf16)
+// The MGM head bank (transformer.py:33-60): C[M][N/2] = GLU(A[M][K] . W[N][K]^T + bias), N = heads x
+// 768 (~49 k), K = 768, M = rows: one 174-GFLOP GEMM per predict.  The 64 x 192 tile above
+// re-reads W once per 64 rows (2.7 GB of L2 traffic at PAD-UFES size); this tile is 128 rows x
+// 256 W rows per 512-thread block (8 waves as 2 x 4, each 64 x 64 = 4 x 4 MFMA-16 tiles),
+// K staged in 64-wide slices, double buffered (one barrier per slice), and blocks that share a
+// W tile are scheduled on one XCD back to back so the tile is fetched from HBM about once.
+// GLU pairs: W rows interleaved in 16-row blocks [a | b] (capi.cpp), so tiles 2q / 2q+1 of a
+// wave are the a / b halves of the same 16 output columns.
+constexpr int GB_M = 128, GB_N = 256, GB_K = 64;
+constexpr int GB_ROWB = 160;                        // LDS bytes per staged row (conflict-free, as above)
+constexpr int GB_STAGE = (GB_M + GB_N) * GB_ROWB;   // 61440
+constexpr int GB_OST = GB_N / 2 + 8;                // output staging row stride (bf16)
+
+__global__ __launch_bounds__(512, 1) void gemm_glu_big_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                                              const float* __restrict__ bias, bf16* __restrict__ C,
+                                                              int M, int N, int K, int mtiles) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fg = lane >> 4;
+  // XCD-aware tile order: XCD x (= block % 8) runs W tiles x, x+8, ..., each for all M tiles in turn
+  int mt, nt;
+  {
+    const int ntiles = N / GB_N, nb = gridDim.x;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int per = nb >> 3, extra = nb & 7;  // blocks per XCD: per (+1 for the first `extra`)
+    const int t = xcd * per + min(xcd, extra) + slot;  // contiguous task range per XCD
+    nt = t / mtiles, mt = t - nt * mtiles;
+    if (nt >= ntiles) return;
+  }
+  const int m0 = mt * GB_M, n0 = nt * GB_N;
+  // staging: A 128 rows x 8 chunks (2 per thread), W 256 rows x 8 chunks (4 per thread), loaded
+  // during the previous slice's MFMAs (a second register set measured no faster and spills)
+  u32x4 ra[2], rw[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 512 * i, r = c >> 3, ch = c & 7;
+      const int m = min(m0 + r, M - 1);
+      ra[i] = *(const u32x4*)(A + (int64_t)m * K + k0 + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 512 * i, r = c >> 3, ch = c & 7;
+      rw[i] = *(const u32x4*)(W + (int64_t)(n0 + r) * K + k0 + ch * 8);
+    }
+  };
+  auto lstore = [&](int buf) {
+    unsigned char* As = smem + buf * GB_STAGE;
+    unsigned char* Ws = As + GB_M * GB_ROWB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 512 * i;
+      *(u32x4*)(As + (c >> 3) * GB_ROWB + (c & 7) * 16) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 512 * i;
+      *(u32x4*)(Ws + (c >> 3) * GB_ROWB + (c & 7) * 16) = rw[i];
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / GB_K;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload((kt + 1) * GB_K);
+    const unsigned char* As = smem + (kt & 1) * GB_STAGE;
+    const unsigned char* Ws = As + GB_M * GB_ROWB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bw[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i] = *(const bf16x8*)(As + (wm * 64 + i * 16 + fr) * GB_ROWB + ks * 64 + fg * 16);
+        bw[i] = *(const bf16x8*)(Ws + (wn * 64 + i * 16 + fr) * GB_ROWB + ks * 64 + fg * 16);
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bw[b], acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < nk) lstore((kt + 1) & 1);
+    __syncthreads();
+  }
+  // GLU epilogue: C tile lane layout (row 16a + 4fg + r, column fr of tile b); a = tile 2q, b = 2q+1
+  bf16* Ct = (bf16*)smem;  // [128][GB_OST] (the last barrier retired every read of the stages)
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int na = n0 + wn * 64 + q * 32 + fr;
+      const float ba = bias[na], bb = bias[na + 16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float va = acc[a][2 * q][r] + ba, vb = acc[a][2 * q + 1][r] + bb;
+        Ct[(wm * 64 + a * 16 + fg * 4 + r) * GB_OST + wn * 32 + q * 16 + fr] = (bf16)(va * sigmoidf_(vb));
+      }
+    }
+  __syncthreads();
+  const int ldc = N / 2, c0 = n0 / 2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // 128 rows x 16 chunks of 16 B
+    const int u = tid + 512 * i, r = u >> 4, ch = u & 15;
+    if (m0 + r < M) *(u32x4*)(C + (int64_t)(m0 + r) * ldc + c0 + ch * 8) = *(const u32x4*)(Ct + r * GB_OST + ch * 8);
+  }
+}
+
 }  // namespace
 
 hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool out_f32, int groups,
@@ -365,6 +480,19 @@ hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool ou
     return out_f32 ? launch_e<true, true, true>(a, epi, groups, st) : launch_e<true, true, false>(a, epi, groups, st);
   }
   return out_f32 ? launch_e<true, false, true>(a, epi, groups, st) : launch_e<true, false, false>(a, epi, groups, st);
+}
+
+hipError_t launch_gemm_glu_big(const void* A, const void* W, const float* bias, void* C, int M, int N, int K,
+                               hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (N % GB_N != 0 || K % GB_K != 0 || K <= 0) return hipErrorInvalidValue;
+  const int mtiles = (M + GB_M - 1) / GB_M;
+  const int64_t nb = (int64_t)mtiles * (N / GB_N);
+  const int lds = 2 * GB_STAGE;
+  static_assert(GB_M * GB_OST * 2 <= 2 * GB_STAGE, "output staging fits the stages");
+  hipLaunchKernelGGL(gemm_glu_big_kernel, dim3((unsigned)nb), dim3(512), lds, st, (const bf16*)A, (const bf16*)W,
+                     bias, (bf16*)C, M, N, K, mtiles);
+  return hipGetLastError();
 }
 
 }  // namespace mmpfn

@@ -50,6 +50,11 @@ struct GemmArgs {
 hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool out_f32, int groups,
                        hipStream_t st);
 
+// MGM head bank, bf16: C[M][N/2] = GLU(A[M][K] . W^T + bias) with W rows GLU-interleaved in 16-row
+// blocks (capi.cpp); large-tile, XCD-ordered (gemm.hip gemm_glu_big_kernel); N % 256 == 0, K % 64 == 0
+hipError_t launch_gemm_glu_big(const void* A, const void* W, const float* bias, void* C, int M, int N, int K,
+                               hipStream_t st);
+
 // fused MLP sublayer: X <- LN(X + GELU(X W1^T) W2^T), W1 [Fh][E], W2 [E][Fh] in compute dtype
 hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M, int E, int Fh, float eps, int prec,
                             hipStream_t st);
