@@ -76,17 +76,35 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ 
 // queries q [cap][E] (in-projected, shared by all rows) and k/v = kv[s][j][0:E] /
 // kv[s][j][E:2E] for the M mixer tokens.  One block per row with one thread per
 // (head, query) pair (cap^2 <= 1024; larger cap loops); the row's keys are staged through
-// LDS once per chunk of up to 64 keys (all M = 64 at mgm 64) and consumed in 32-key
+// LDS once per chunk of up to 64 keys (all M = 64 at mgm 64; bf16 keys stay bf16 in LDS, 49 KB,
+// so three rows' blocks share a CU) and consumed in 32-key
 // register sub-chunks by a chunked online softmax in fp32 (exp2 with log2(e) folded into
 // the query scale).  HD (head dim = E / cap) is a template parameter so the per-thread
 // q / acc arrays stay in registers.
 constexpr int CAP_KC = 32;
 constexpr int CAP_STAGE = 64;
 
+// HD-wide row of K or V from LDS as fp32 (bf16 rows: 16-B reads when HD % 8 == 0)
+template <typename TK, int HD>
+__device__ __forceinline__ void cap_row(const TK* r, float (&o)[HD]) {
+  if constexpr (sizeof(TK) == 2 && HD % 8 == 0) {
+#pragma unroll
+    for (int c = 0; c < HD / 8; ++c) {
+      const bf16x8 v = *(const bf16x8*)(r + 8 * c);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[8 * c + i] = (float)v[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < HD; ++i) o[i] = to_f32(r[i]);
+  }
+}
+
 template <typename TK, int HD>
 __global__ __launch_bounds__(1024) void cap_attn_kernel(const float* __restrict__ qp, const TK* __restrict__ kv,
                                                         float* __restrict__ out, int M, int cap, int E, int kcmax) {
-  extern __shared__ float ks[];  // [kcmax][2E], kcmax <= CAP_STAGE
+  extern __shared__ __attribute__((aligned(16))) unsigned char cap_lds[];
+  TK* ks = (TK*)cap_lds;  // [kcmax][2E] in the storage type (bf16: 49 KB at M = 64, E = 192)
   const int s = blockIdx.x;
   const int tid = threadIdx.x, nt = blockDim.x;
   const float scale = 1.4426950408889634f / sqrtf((float)HD);
@@ -108,7 +126,12 @@ __global__ __launch_bounds__(1024) void cap_attn_kernel(const float* __restrict_
     for (int k0 = 0; k0 < M; k0 += kcmax) {
       const int kc = min(kcmax, M - k0);
       __syncthreads();
-      for (int i = tid; i < kc * 2 * E; i += nt) ks[i] = to_f32(kvs[(int64_t)k0 * 2 * E + i]);
+      {  // 16-B copies (2E * sizeof(TK) per key is a multiple of 16: E % 4 == 0 checked at launch)
+        const int n16 = kc * 2 * E * (int)sizeof(TK) / 16;
+        const u32x4* src = (const u32x4*)(kvs + (int64_t)k0 * 2 * E);
+        u32x4* dst = (u32x4*)ks;
+        for (int i = tid; i < n16; i += nt) dst[i] = src[i];
+      }
       __syncthreads();
       if (!active) continue;
       for (int j0 = 0; j0 < kc; j0 += CAP_KC) {
@@ -119,7 +142,8 @@ __global__ __launch_bounds__(1024) void cap_attn_kernel(const float* __restrict_
         for (int kk = 0; kk < CAP_KC; ++kk) {
           float a = -INFINITY;
           if (kk < jc) {
-            const float* kr = ks + (j0 + kk) * 2 * E + h * HD;
+            float kr[HD];
+            cap_row<TK, HD>(ks + (j0 + kk) * 2 * E + h * HD, kr);
             a = 0.f;
 #pragma unroll
             for (int i = 0; i < HD; ++i) a = fmaf(q[i], kr[i], a);
@@ -137,7 +161,8 @@ __global__ __launch_bounds__(1024) void cap_attn_kernel(const float* __restrict_
           if (kk < jc) {
             const float pe = __builtin_amdgcn_exp2f(sc[kk] - mn);
             l += pe;
-            const float* vr = ks + (j0 + kk) * 2 * E + E + h * HD;
+            float vr[HD];
+            cap_row<TK, HD>(ks + (j0 + kk) * 2 * E + E + h * HD, vr);
 #pragma unroll
             for (int i = 0; i < HD; ++i) acc[i] = fmaf(pe, vr[i], acc[i]);
           }
@@ -233,9 +258,10 @@ hipError_t launch_layernorm_rows(const float* in, int64_t rows, int dim, float e
 
 template <typename TK>
 hipError_t launch_cap_t(const float* qp, const TK* kv, float* out, int S, int M, int cap, int E, hipStream_t st) {
-  // the row's keys staged (fp32) in chunks of up to 64 keys, within 96 KiB of LDS
-  const int kcmax = max(1, min(CAP_STAGE, 98304 / (8 * E)));
-  const size_t lds = (size_t)kcmax * 2 * E * sizeof(float);
+  // the row's keys staged in their storage type, chunks of up to 64 keys within 96 KiB of LDS
+  if (E % 4 != 0) return hipErrorInvalidValue;
+  const int kcmax = max(1, min(CAP_STAGE, 98304 / (2 * E * (int)sizeof(TK))));
+  const size_t lds = (size_t)kcmax * 2 * E * sizeof(TK);
   const int pairs = cap * cap;
   dim3 g(S), b((unsigned)min(1024, (pairs + 63) / 64 * 64));
   switch (E / cap) {
