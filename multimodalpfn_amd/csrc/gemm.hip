@@ -352,16 +352,32 @@ hipError_t launch_e(const GemmArgs& a, int epi, int groups, hipStream_t st) {
 // ---------------------------------------------------------------- large-tile GLU GEMM (bf16)
 // The MGM head bank (transformer.py:33-60): C[M][N/2] = GLU(A[M][K] . W[N][K]^T + bias), N = heads x
 // 768 (~49 k), K = 768, M = rows: one 174-GFLOP GEMM per predict.  The 64 x 192 tile above
-// re-reads W once per 64 rows (2.7 GB of L2 traffic at PAD-UFES size); this tile is 128 rows x
-// 256 W rows per 512-thread block (8 waves as 2 x 4, each 64 x 64 = 4 x 4 MFMA-16 tiles),
-// K staged in 64-wide slices, double buffered (one barrier per slice), and blocks that share a
-// W tile are scheduled on one XCD back to back so the tile is fetched from HBM about once.
+// re-reads W once per 64 rows (2.7 GB of L2 traffic at PAD-UFES size); this tile is 256 rows x
+// 256 W rows per 512-thread block (8 waves as 2 x 4, each 128 x 64 = 8 x 4 MFMA-16 tiles), and
+// blocks that share a W tile are scheduled on one XCD back to back so the tile is fetched from
+// HBM about once.  K moves in 32-wide slices through a 4-stage LDS ring filled by LDS-DMA
+// (global_load_lds_dwordx4: no staging registers, no LDS write pass after the MFMAs): slice
+// kt+1..kt+3 are in flight while slice kt computes; one barrier per slice.  LDS images are unpadded
+// 64-B rows with 16-B chunk c of row r at slot c ^ ((r >> 1) & 3) (conflict-free ds_read_b128 for
+// the 16x16x32 operands); the DMA writes lane-linear, so each lane fetches the chunk that belongs
+// at its slot.  The DMA is inline asm so the compiler adds no vmcnt(0) before the LDS reads of
+// the other stages; the kernel waits for its own slices explicitly.
 // GLU pairs: W rows interleaved in 16-row blocks [a | b] (capi.cpp), so tiles 2q / 2q+1 of a
 // wave are the a / b halves of the same 16 output columns.
-constexpr int GB_M = 128, GB_N = 256, GB_K = 64;
-constexpr int GB_ROWB = 160;                        // LDS bytes per staged row (conflict-free, as above)
-constexpr int GB_STAGE = (GB_M + GB_N) * GB_ROWB;   // 61440
+constexpr int GB_M = 256, GB_N = 256, GB_K = 32;
+constexpr int GB_ROW = GB_K * 2;                    // 64-B LDS rows
+constexpr int GB_STAGE = (GB_M + GB_N) * GB_ROW;    // 32 KB
+constexpr int GB_NST = 4;                           // ring stages (128 KB)
 constexpr int GB_OST = GB_N / 2 + 8;                // output staging row stride (bf16)
+constexpr int GB_DMA = (GB_M + GB_N) * (GB_ROW / 16) / 512;  // 16-B DMA pieces per thread and slice (4)
+constexpr int GB_MT = GB_M / 32;                    // 16-row MFMA tiles per wave (8)
+
+__device__ __forceinline__ int gb_slot(int r, int c) { return c ^ ((r >> 1) & 3); }
+
+__device__ __forceinline__ void gb_dma16(const void* src, unsigned lds_base) {
+  // m0 = the wave's LDS destination; lane i's 16 B land at m0 + 16 i
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_base) : "memory");
+}
 
 __global__ __launch_bounds__(512, 1) void gemm_glu_big_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                               const float* __restrict__ bias, bf16* __restrict__ C,
@@ -370,95 +386,89 @@ __global__ __launch_bounds__(512, 1) void gemm_glu_big_kernel(const bf16* __rest
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int fr = lane & 15, fg = lane >> 4;
-  // XCD-aware tile order: XCD x (= block % 8) runs W tiles x, x+8, ..., each for all M tiles in turn
+  // XCD-aware tile order: XCD x (= block % 8) runs a contiguous range of (W tile, M tile) tasks,
+  // W-tile-major, so the M tiles of one W tile run back to back on one L2
   int mt, nt;
   {
-    const int ntiles = N / GB_N, nb = gridDim.x;
+    const int nb = gridDim.x;
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    const int per = nb >> 3, extra = nb & 7;  // blocks per XCD: per (+1 for the first `extra`)
-    const int t = xcd * per + min(xcd, extra) + slot;  // contiguous task range per XCD
+    const int per = nb >> 3, extra = nb & 7;
+    const int t = xcd * per + min(xcd, extra) + slot;
     nt = t / mtiles, mt = t - nt * mtiles;
-    if (nt >= ntiles) return;
   }
   const int m0 = mt * GB_M, n0 = nt * GB_N;
-  // staging: A 128 rows x 8 chunks (2 per thread), W 256 rows x 8 chunks (4 per thread), loaded
-  // during the previous slice's MFMAs (a second register set measured no faster and spills)
-  u32x4 ra[2], rw[4];
-  auto gload = [&](int k0) {
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
+
+  // DMA piece j of this wave: LDS chunk q = (wave * GB_DMA + j) * 64 + lane of the stage image
+  // (rows 0-255 = A, 256-511 = W); row r = q / 4 holds global chunk c with gb_slot(r, c) = q % 4
+  const bf16* src[GB_DMA];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 512 * i, r = c >> 3, ch = c & 7;
-      const int m = min(m0 + r, M - 1);
-      ra[i] = *(const u32x4*)(A + (int64_t)m * K + k0 + ch * 8);
-    }
+  for (int j = 0; j < GB_DMA; ++j) {
+    const int q = (wave * GB_DMA + j) * 64 + lane, r = q >> 2, c = gb_slot(r, q & 3);
+    src[j] = r < GB_M ? A + (int64_t)min(m0 + r, M - 1) * K + c * 8 : W + (int64_t)(n0 + r - GB_M) * K + c * 8;
+  }
+  auto dma = [&](int kt) {
+    const unsigned base = lds0 + (kt % GB_NST) * GB_STAGE + wave * GB_DMA * 1024;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 512 * i, r = c >> 3, ch = c & 7;
-      rw[i] = *(const u32x4*)(W + (int64_t)(n0 + r) * K + k0 + ch * 8);
-    }
+    for (int j = 0; j < GB_DMA; ++j)
+      gb_dma16(src[j] + kt * GB_K, __builtin_amdgcn_readfirstlane(base + j * 1024));
   };
-  auto lstore = [&](int buf) {
-    unsigned char* As = smem + buf * GB_STAGE;
-    unsigned char* Ws = As + GB_M * GB_ROWB;
+  f32x4 acc[GB_MT][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 512 * i;
-      *(u32x4*)(As + (c >> 3) * GB_ROWB + (c & 7) * 16) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 512 * i;
-      *(u32x4*)(Ws + (c >> 3) * GB_ROWB + (c & 7) * 16) = rw[i];
-    }
-  };
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < GB_MT; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / GB_K;
-  gload(0);
-  lstore(0);
-  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < GB_NST - 1; ++i)
+    if (i < nk) dma(i);
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload((kt + 1) * GB_K);
-    const unsigned char* As = smem + (kt & 1) * GB_STAGE;
-    const unsigned char* Ws = As + GB_M * GB_ROWB;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bw[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        af[i] = *(const bf16x8*)(As + (wm * 64 + i * 16 + fr) * GB_ROWB + ks * 64 + fg * 16);
-        bw[i] = *(const bf16x8*)(Ws + (wn * 64 + i * 16 + fr) * GB_ROWB + ks * 64 + fg * 16);
-      }
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bw[b], acc[a][b], 0, 0, 0);
-    }
-    if (kt + 1 < nk) lstore((kt + 1) & 1);
+    // this thread's pieces of slice kt have landed (up to two later slices may still fly)
+    const int ahead = min(nk - 1 - kt, GB_NST - 2);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GB_DMA) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB_DMA) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // stage (kt+3) % 4 was last read in slice kt-1, before the barrier above
+    if (kt + GB_NST - 1 < nk) dma(kt + GB_NST - 1);
+    const unsigned char* As = smem + (kt % GB_NST) * GB_STAGE;
+    const unsigned char* Ws = As + GB_M * GB_ROW;
+    bf16x8 af[GB_MT], bw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rb = wn * 64 + i * 16 + fr;
+      bw[i] = *(const bf16x8*)(Ws + rb * GB_ROW + 16 * gb_slot(rb, fg));
+    }
+#pragma unroll
+    for (int i = 0; i < GB_MT; ++i) {
+      const int ra = wm * (GB_M / 2) + i * 16 + fr;
+      af[i] = *(const bf16x8*)(As + ra * GB_ROW + 16 * gb_slot(ra, fg));
+    }
+#pragma unroll
+    for (int a = 0; a < GB_MT; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bw[b], acc[a][b], 0, 0, 0);
   }
+  __syncthreads();  // every wave is done with the ring before it is reused for the output tile
   // GLU epilogue: C tile lane layout (row 16a + 4fg + r, column fr of tile b); a = tile 2q, b = 2q+1
-  bf16* Ct = (bf16*)smem;  // [128][GB_OST] (the last barrier retired every read of the stages)
+  bf16* Ct = (bf16*)smem;  // [GB_M][GB_OST]
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int q = 0; q < 2; ++q) {
+    const int na = n0 + wn * 64 + q * 32 + fr;
+    const float ba = bias[na], bb = bias[na + 16];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int na = n0 + wn * 64 + q * 32 + fr;
-      const float ba = bias[na], bb = bias[na + 16];
+    for (int a = 0; a < GB_MT; ++a)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float va = acc[a][2 * q][r] + ba, vb = acc[a][2 * q + 1][r] + bb;
-        Ct[(wm * 64 + a * 16 + fg * 4 + r) * GB_OST + wn * 32 + q * 16 + fr] = (bf16)(va * sigmoidf_(vb));
+        Ct[(wm * (GB_M / 2) + a * 16 + fg * 4 + r) * GB_OST + wn * 32 + q * 16 + fr] = (bf16)(va * sigmoidf_(vb));
       }
-    }
+  }
   __syncthreads();
   const int ldc = N / 2, c0 = n0 / 2;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {  // 128 rows x 16 chunks of 16 B
+  for (int i = 0; i < GB_M * 16 / 512; ++i) {  // GB_M rows x 16 chunks of 16 B
     const int u = tid + 512 * i, r = u >> 4, ch = u & 15;
     if (m0 + r < M) *(u32x4*)(C + (int64_t)(m0 + r) * ldc + c0 + ch * 8) = *(const u32x4*)(Ct + r * GB_OST + ch * 8);
   }
@@ -488,8 +498,8 @@ hipError_t launch_gemm_glu_big(const void* A, const void* W, const float* bias, 
   if (N % GB_N != 0 || K % GB_K != 0 || K <= 0) return hipErrorInvalidValue;
   const int mtiles = (M + GB_M - 1) / GB_M;
   const int64_t nb = (int64_t)mtiles * (N / GB_N);
-  const int lds = 2 * GB_STAGE;
-  static_assert(GB_M * GB_OST * 2 <= 2 * GB_STAGE, "output staging fits the stages");
+  const int lds = GB_NST * GB_STAGE;  // 144 KB
+  static_assert(GB_M * GB_OST * 2 <= GB_NST * GB_STAGE, "output staging fits the ring");
   hipLaunchKernelGGL(gemm_glu_big_kernel, dim3((unsigned)nb), dim3(512), lds, st, (const bf16*)A, (const bf16*)W,
                      bias, (bf16*)C, M, N, K, mtiles);
   return hipGetLastError();
