@@ -734,11 +734,16 @@ int mixer(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, i
     RC(ensure(ctx, ctx->mx[5], (size_t)S * cap * E * 4));       // attention out (heads concat)
     RC(ensure(ctx, ctx->mx[6], (size_t)S * cap * E * 4));       // out_proj
     RC(ensure(ctx, ctx->mx[7], (size_t)S * cap * 2 * E * 4));   // ffn hidden (+ ffn out after)
-    HIPCHK(launch_layernorm_rows(mtok, srows, E, 1e-5f, ctx->mx[3].p, !bf, nullptr, nullptr, st));
-    GemmArgs c = gargs();
-    c.A = ctx->mx[3].p, c.lda = E, c.W = W(ctx->cap_kv, ctx->cap_kv_h, prec), c.bias = (const float*)ctx->cap_kv_b.p;
-    c.M = (int)srows, c.N = 2 * E, c.K = E, c.C = ctx->mx[4].p, c.ldc = 2 * E;
-    HIPCHK(launch_gemm(c, prec, EPI_STORE, !bf, !bf, 1, st));
+    if (bf && E == 192) {  // k_norm + K|V projection in one row pass (normalised rows stay in registers)
+      HIPCHK(launch_rowgemm_ln_store(mtok, ctx->cap_kv_h.p, (const float*)ctx->cap_kv_b.p, ctx->mx[4].p, srows, 2 * E,
+                                     1e-5f, true, st));
+    } else {
+      HIPCHK(launch_layernorm_rows(mtok, srows, E, 1e-5f, ctx->mx[3].p, !bf, nullptr, nullptr, st));
+      GemmArgs c = gargs();
+      c.A = ctx->mx[3].p, c.lda = E, c.W = W(ctx->cap_kv, ctx->cap_kv_h, prec), c.bias = (const float*)ctx->cap_kv_b.p;
+      c.M = (int)srows, c.N = 2 * E, c.K = E, c.C = ctx->mx[4].p, c.ldc = 2 * E;
+      HIPCHK(launch_gemm(c, prec, EPI_STORE, !bf, !bf, 1, st));
+    }
     HIPCHK(launch_cap_attention((const float*)ctx->cap_qp.p, ctx->mx[4].p, !bf, (float*)ctx->mx[5].p, S, M, cap, E,
                                 st));
     const int64_t crow = (int64_t)S * cap;

@@ -74,6 +74,9 @@ hipError_t launch_mlp_rows(float* X, const void* W1perm, const void* W2perm, int
 hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
                               const void* W, int M, int N, void* q, void* k, void* vt, int S, int Npad, int H,
                               hipStream_t st);
+// C = (ln ? LayerNorm(A) : A) . W^T + bias: A fp32 [M][192], W [N][192] bf16, C bf16 [M][N], N % 64 == 0
+hipError_t launch_rowgemm_ln_store(const float* A, const void* W, const float* bias, void* C, int64_t M, int N,
+                                   float eps, bool ln, hipStream_t st);
 hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, float* X, float eps, hipStream_t st);
 
 // row-resident attention-between-features sublayer (bf16 only, featrow.hip): one wave per

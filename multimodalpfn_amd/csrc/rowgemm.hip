@@ -285,6 +285,106 @@ __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p, in
   }
 }
 
+// C[m] = (LN? LayerNorm(A[m]) : A[m]) . W^T + bias, A fp32 [M][192], W [N][192] bf16, C bf16 [M][N]
+// (N % 64 == 0): the CAP K|V projection of the normalised mixer tokens (transformer.py:77-84) in
+// one pass -- the LayerNorm (no affine; folded into W on the host) runs on the rows in registers,
+// so the normalised copy never reaches HBM.  Same chunk pipeline and LDS-staged 16-B stores as
+// the QKV kernel above.
+__global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const float* __restrict__ A, const bf16* __restrict__ W,
+                                                                  const float* __restrict__ bias, bf16* __restrict__ C,
+                                                                  int M, int N, float eps, int do_ln) {
+  __shared__ __attribute__((aligned(16))) bf16 Ws[2 * QCEL + 4 * OWEL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * GROWS + wave * 32;
+  bf16* const Os = Ws + 2 * QCEL + wave * OWEL;
+  const int nch = N / QC;
+  u32x4 r[QCP];
+  auto fetch = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < QCP; ++j) {
+      const int i = tid + 256 * j;
+      r[j] = *(const u32x4*)(W + (int64_t)(c * QC + i / (GE / 8)) * GE + (i % (GE / 8)) * 8);
+    }
+  };
+  auto stash = [&](int slot) {
+#pragma unroll
+    for (int j = 0; j < QCP; ++j) {
+      const int i = tid + 256 * j;
+      *(u32x4*)(Ws + slot * QCEL + (i / (GE / 8)) * WST + (i % (GE / 8)) * 8) = r[j];
+    }
+  };
+  fetch(0);
+  bf16x8 af[2][GE / 32];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
+    const float* xr = A + m * GE + fg * 8;
+    f32x4 lo[GE / 32], hi[GE / 32];
+#pragma unroll
+    for (int ks = 0; ks < GE / 32; ++ks) {
+      lo[ks] = *(const f32x4*)(xr + ks * 32);
+      hi[ks] = *(const f32x4*)(xr + ks * 32 + 4);
+    }
+    float mean = 0.f, inv = 1.f;
+    if (do_ln) {  // the row's 192 features are spread over lanes fr + 16 fg (48 each)
+      float sm = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < GE / 32; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sm += lo[ks][i] + hi[ks][i];
+      mean = sum_rows4(sm) * (1.0f / GE);
+      float q = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < GE / 32; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float a = lo[ks][i] - mean, b = hi[ks][i] - mean;
+          q += a * a + b * b;
+        }
+      inv = 1.0f / sqrtf(sum_rows4(q) * (1.0f / GE) + eps);
+    }
+#pragma unroll
+    for (int ks = 0; ks < GE / 32; ++ks) {
+      bf16x8 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (bf16)((lo[ks][i] - mean) * inv), v[4 + i] = (bf16)((hi[ks][i] - mean) * inv);
+      af[tt][ks] = v;
+    }
+  }
+  stash(0);
+  if (nch > 1) fetch(1);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) stash((c + 1) & 1);
+    if (c + 2 < nch) fetch(c + 2);
+    const bf16* Wc = Ws + (c & 1) * QCEL;
+    f32x4 acc[QC / 16][2];
+#pragma unroll
+    for (int f = 0; f < QC / 16; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    chunk_mma<true>(Wc, af, fr, fg, acc);
+    // C^T: lane = row 16tt + fr, features 16f + 4fg + i  ->  Os[row][feature] (+ bias)
+#pragma unroll
+    for (int f = 0; f < QC / 16; ++f) {
+      const f32x4 bv = *(const f32x4*)(bias + c * QC + f * 16 + fg * 4);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (bf16)(acc[f][tt][i] + bv[i]);
+        *(bf16x4*)(Os + (tt * 16 + fr) * OQST + f * 16 + fg * 4) = o;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // 32 rows x 8 chunks of 16 B
+      const int row = 8 * i + (lane >> 3), cc = lane & 7;
+      const u32x4 v = *(const u32x4*)(Os + row * OQST + cc * 8);
+      if (m0 + row < M) *(u32x4*)(C + (m0 + row) * N + c * QC + cc * 8) = v;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256, 2) void rowgemm_resln_kernel(const RgArgs p) {
   __shared__ __attribute__((aligned(16))) bf16 Ws[GE * WST];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -362,6 +462,15 @@ hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, float* 
   a.A = O, a.a_rdiv = 1, a.a_rmul = 1, a.a_rmul2 = 0, a.a_roff = 0;
   a.W = (const bf16*)W, a.M = (int)M, a.N = GE, a.X = X, a.eps = eps;
   hipLaunchKernelGGL(rowgemm_resln_kernel, dim3((unsigned)((M + GROWS - 1) / GROWS)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rowgemm_ln_store(const float* A, const void* W, const float* bias, void* C, int64_t M, int N,
+                                   float eps, bool ln, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (N % QC != 0 || N <= 0 || M > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rowgemm_ln_store_kernel, dim3((unsigned)((M + GROWS - 1) / GROWS)), dim3(256), 0, st, A,
+                     (const bf16*)W, bias, (bf16*)C, (int)M, N, eps, ln ? 1 : 0);
   return hipGetLastError();
 }
 
