@@ -161,31 +161,28 @@ __global__ __launch_bounds__(1024) void enc_x_stats_kernel(const float* __restri
 }
 
 // EMB_TOK tokens per block: the per-token model inputs (u, NaN/inf indicators) are computed
-// once per (token, slot) into LDS next to the encoder weights and each token's
-// positional-embedding row; then one thread per (token, 4 embedding columns)
-// writes the embedding from LDS operands (contiguous 16-B stores over the block's tokens)
-constexpr int EMB_TOK = 16;
+// once per (token, slot) into LDS next to the encoder weights; then each thread writes 16-B
+// pieces of the embedding (4 columns of one token, consecutive threads -> consecutive columns),
+// adding the token's group positional row straight from global memory (one 768-B row per group,
+// cache resident).  64 tokens per block: one block round at PAD-UFES size instead of a
+// latency-bound stream of 16-token blocks.
+constexpr int EMB_TOK = 64;
 constexpr int EMB_EMAX = 256;
 __global__ __launch_bounds__(256) void enc_x_embed_kernel(const float* __restrict__ x, int S, int F, int G, int fpg,
                                                           int nf, const SlotParams* __restrict__ slots,
                                                           const float* __restrict__ w, const float* __restrict__ pe,
                                                           float* __restrict__ X, int E, int* flag) {
   __shared__ float su[EMB_TOK][8], si[EMB_TOK][8];
-  __shared__ float ws[EMB_EMAX * 16], ps[EMB_TOK][EMB_EMAX];
+  __shared__ float ws[EMB_EMAX * 16];
   const int tid = threadIdx.x, nin = 2 * nf;
   const int64_t ntok = (int64_t)S * G, tok0 = (int64_t)blockIdx.x * EMB_TOK;
   for (int i = tid; i < E * nin; i += blockDim.x) ws[i] = w[i];
-  for (int i = tid; i < EMB_TOK * E; i += blockDim.x) {  // positional-embedding row of each token's group
-    const int t = i / E, e = i - t * E;
-    const int64_t tok = tok0 + t;
-    ps[t][e] = tok < ntok ? pe[(tok / S) * E + e] : 0.f;
-  }
-  if (tid < EMB_TOK * 8) {
-    const int i = tid >> 3, k = tid & 7;
+  for (int it = tid; it < EMB_TOK * 8; it += blockDim.x) {
+    const int i = it >> 3, k = it & 7;
     const int64_t tok = tok0 + i;
     float u = 0.f, ind = 0.f;
     if (tok < ntok && k < fpg) {
-      const int g = (int)(tok / S), s = (int)(tok - (int64_t)g * S);
+      const int g = (int)tok / S, s = (int)tok - g * S;
       const SlotParams p = slots[g * fpg + k];
       float used = 0.f;  // used-feature rescale sqrt(nf / used) of the group (encoders.py:608-655)
       for (int j = 0; j < fpg; ++j) used += slots[g * fpg + j].scale;
@@ -208,6 +205,7 @@ __global__ __launch_bounds__(256) void enc_x_embed_kernel(const float* __restric
     const int i = item / E4, e4 = item - i * E4;
     const int64_t tok = tok0 + i;
     if (tok >= ntok) break;
+    const f32x4 pv = *(const f32x4*)(pe + (int)((int)tok / S) * E + e4 * 4);  // S * G < 2^31 (launcher)
     f32x4 o;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -216,7 +214,7 @@ __global__ __launch_bounds__(256) void enc_x_embed_kernel(const float* __restric
       float a = 0.f;
       for (int k = 0; k < nf; ++k) a = fmaf(su[i][k], wr[k], a);
       for (int k = 0; k < nf; ++k) a = fmaf(si[i][k], wr[nf + k], a);
-      a += ps[i][e];
+      a += pv[c];
       o[c] = a;
       nan_seen |= isnan(a);
     }
@@ -436,7 +434,7 @@ hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, 
   if (fpg > 8 || nf > 8 || nf < fpg) return hipErrorInvalidValue;
   if (stats)
     hipLaunchKernelGGL(enc_x_stats_kernel, dim3(G, fpg), dim3(1024), 0, st, x, S, F, N, fpg, nf, sigma, slots);
-  if (fpg > 8 || nf > 8 || E > EMB_EMAX) return hipErrorInvalidValue;
+  if (fpg > 8 || nf > 8 || E > EMB_EMAX || E % 4 != 0 || (int64_t)S * G >= INT32_MAX) return hipErrorInvalidValue;
   const int64_t nblk = ((int64_t)S * G + EMB_TOK - 1) / EMB_TOK;
   hipLaunchKernelGGL(enc_x_embed_kernel, dim3((unsigned)nblk), dim3(256), 0, st, x, S, F, G, fpg, nf, slots, w_enc,
                      posemb, X, E, flag);
