@@ -164,9 +164,9 @@ __global__ __launch_bounds__(1024) void enc_x_stats_kernel(const float* __restri
 // once per (token, slot) into LDS next to the encoder weights; then each thread writes 16-B
 // pieces of the embedding (4 columns of one token, consecutive threads -> consecutive columns),
 // adding the token's group positional row straight from global memory (one 768-B row per group,
-// cache resident).  64 tokens per block: one block round at PAD-UFES size instead of a
-// latency-bound stream of 16-token blocks.
-constexpr int EMB_TOK = 64;
+// cache resident).  16 tokens per block (64 measured 31 vs 33 us alone but 53 vs 46 us beside the
+// other lane's kernels in the bench: small blocks share the CUs better).
+constexpr int EMB_TOK = 16;
 constexpr int EMB_EMAX = 256;
 __global__ __launch_bounds__(256) void enc_x_embed_kernel(const float* __restrict__ x, int S, int F, int G, int fpg,
                                                           int nf, const SlotParams* __restrict__ slots,
