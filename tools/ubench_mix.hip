@@ -50,6 +50,17 @@ __global__ void kern(float* out, int iters) {
       }
       continue;
     }
+    if constexpr (XV == 6) {  // 8 x 16x16x32 (same flops as 4 x 32x32x16) + the exps
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f32x4 t = {acc[j & 3][4 * (j >> 2)], acc[j & 3][4 * (j >> 2) + 1], acc[j & 3][4 * (j >> 2) + 2], acc[j & 3][4 * (j >> 2) + 3]};
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, t, 0, 0, 0);
+        acc[j & 3][4 * (j >> 2)] = t[0], acc[j & 3][4 * (j >> 2) + 1] = t[1], acc[j & 3][4 * (j >> 2) + 2] = t[2], acc[j & 3][4 * (j >> 2) + 3] = t[3];
+      }
+#pragma unroll
+      for (int j = 0; j < NE / 16; ++j) E16;
+      continue;
+    }
     if constexpr (XV == 5) {  // 16x16x32 MFMAs (4 per 32x32x16 equivalent) interleaved with exps
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
@@ -102,16 +113,18 @@ void run() {
     (void)hipEventElapsedTime(&ms, e0, e1);
     const double wps = (double)blocks * threads / 64 / 1024;
     const double per = ms * 1e-3 / (iters * wps) * 2.0e9;
-    printf("exp%s %s chains %d mfma32 x%d + exp x%2d + cvt x%2d + fma x%2d + pkfma x%2d grid %4dx%3d waves/SIMD %.0f: %6.1f cyc/body/SIMD\n", XV == 0 ? "f32" : XV == 1 ? "f16" : XV == 2 ? "f16sdwa" : XV == 3 ? "f32-il" : XV == 4 ? "f32-il-prio" : "f32-il-16x16", AG ? "agpr" : "vgpr", NA, NM, NE, NC, NF, NP, blocks,
+    printf("exp%s %s chains %d mfma32 x%d + exp x%2d + cvt x%2d + fma x%2d + pkfma x%2d grid %4dx%3d waves/SIMD %.0f: %6.1f cyc/body/SIMD\n", XV == 0 ? "f32" : XV == 1 ? "f16" : XV == 2 ? "f16sdwa" : XV == 3 ? "f32-il" : XV == 4 ? "f32-il-prio" : XV == 5 ? "f32-il-16x16" : "8x16x16x32", AG ? "agpr" : "vgpr", NA, NM, NE, NC, NF, NP, blocks,
            threads, wps, per);
     (void)hipFree(out);
   }
 }
 
 int main() {
+  run<4, 0, 0, 4, false, 0, 0, 0>();
+  run<4, 0, 0, 4, false, 0, 0, 6>();
   run<4, 16, 0, 4, false, 0, 0, 0>();
-  run<4, 16, 0, 4, false, 0, 0, 3>();
-  run<4, 16, 0, 4, false, 0, 0, 4>();
-  run<4, 16, 0, 4, false, 0, 0, 5>();
+  run<4, 16, 0, 4, false, 0, 0, 6>();
+  run<4, 32, 0, 4, false, 0, 0, 0>();
+  run<4, 32, 0, 4, false, 0, 0, 6>();
   return 0;
 }
