@@ -684,12 +684,16 @@ int run_layer(mmpfn_ctx* ctx, int l) {
   return MMPFN_OK;
 }
 
-int decode(mmpfn_ctx* ctx, float* logits, int m = 0) {
+// decoder over the test rows of M batched members (logits [M][Q][n_out]); the tile partials go
+// through the attention-output workspace, free once the last layer has run
+int decode(mmpfn_ctx* ctx, float* logits, int M = 1) {
   const mmpfn_model_desc& d = ctx->d;
-  const int E = d.emsize, S = ctx->S, T = ctx->T, N = ctx->N;
-  const float* Xl = (const float*)ctx->ws_X.p + (size_t)m * S * T * E + ((size_t)(T - 1) * S + N) * E;
-  HIPCHK(launch_decoder(Xl, S - N, (const float*)ctx->dec_w1.p, (const float*)ctx->dec_b1.p, d.nhid,
-                        (const float*)ctx->dec_w2.p, (const float*)ctx->dec_b2.p, d.n_out, logits, E, ctx->stream));
+  const int E = d.emsize, S = ctx->S, T = ctx->T, N = ctx->N, Q = S - N;
+  const float* Xl = (const float*)ctx->ws_X.p + ((size_t)(T - 1) * S + N) * E;
+  RC(ensure(ctx, ctx->ws_O, (size_t)M * (d.nhid / 32 + 1) * Q * d.n_out * sizeof(float)));
+  HIPCHK(launch_decoder(Xl, Q, (const float*)ctx->dec_w1.p, (const float*)ctx->dec_b1.p, d.nhid,
+                        (const float*)ctx->dec_w2.p, (const float*)ctx->dec_b2.p, d.n_out, logits, E, ctx->stream, M,
+                        (int64_t)S * T * E, (int64_t)Q * d.n_out, (float*)ctx->ws_O.p));
   return MMPFN_OK;
 }
 
@@ -960,9 +964,7 @@ int mmpfn_forward_batch(mmpfn_ctx* ctx, int M, const float* const* x, int S, int
   for (int m = 0; m < M; ++m)
     RC(embed(ctx, F > 0 ? x[m] : nullptr, S, F, tokens, C, y[m], N, uniq[m], U[m], pos_rand, precision, m, M));
   for (int l = 0; l < ctx->d.nlayers; ++l) RC(run_layer(ctx, l));
-  const size_t per = (size_t)(S - N) * ctx->d.n_out;
-  for (int m = 0; m < M; ++m) RC(decode(ctx, logits + m * per, m));
-  return MMPFN_OK;
+  return decode(ctx, logits, M);
 }
 
 int mmpfn_state_tokens(const mmpfn_ctx* ctx) { return ctx ? ctx->T : 0; }

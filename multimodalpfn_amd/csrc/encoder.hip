@@ -293,71 +293,74 @@ __global__ __launch_bounds__(256) void add_tokens_kernel(const float* __restrict
   if (isnan(v[0]) || isnan(v[1]) || isnan(v[2]) || isnan(v[3])) atomicOr(flag, 1);
 }
 
-// decoder: Linear(E, Fh) + GELU + Linear(Fh, n_out) on one query row per block
-// decoder MLP (transformer.py:388-403, 850-853): DEC_R query rows per block of 1024 threads.
-// W1 is stored transposed [E][Fh]: thread (kq, o) accumulates k in [kq*E/4, (kq+1)*E/4) for
-// hidden units o, o+256, o+512 with 16 loads in flight (coalesced rows, reused for all DEC_R
-// rows); the four k-quarter partials are summed in order through LDS.  The kernel is bound by
-// load latency (W1 is 0.6 MB per block), so the k split is what shortens it.
-constexpr int DEC_R = 4;
-constexpr int DEC_KQ = 4;
-__global__ __launch_bounds__(1024) void decoder_kernel(const float* __restrict__ X, int Q,
-                                                       const float* __restrict__ w1t,
-                                                       const float* __restrict__ b1, int Fh,
-                                                       const float* __restrict__ w2, const float* __restrict__ b2,
-                                                       int n_out, float* __restrict__ out, int E) {
-  extern __shared__ float sm[];
-  float* xs = sm;                          // [DEC_R][E]
-  float* part = sm + DEC_R * E;            // [DEC_KQ][DEC_R][Fh]
-  float* hs = part;                        // [DEC_R][Fh], reuses quarter 0
-  const int q0 = blockIdx.x * DEC_R, tid = threadIdx.x;
-  for (int i = tid; i < DEC_R * E; i += blockDim.x) {
+// Decoder (transformer.py:388-403,850-853): out = GELU(X W1^T + b1) W2^T + b2 over the Q test rows
+// of M members.  Tiled in two launches: dec_hidden_kernel owns a 32-row x 32-hidden tile (X rows
+// and the W1 column slice in LDS, one thread per hidden unit and 4 rows, exact-erf GELU) and
+// writes that tile's partial outputs [Fh/32][Q][n_out]; dec_sum_kernel adds the partials in a
+// fixed order (+ b2).  A per-4-row block streaming all of W1 (0.6 MB) was bound by one CU's
+// fill rate (27 us alone, 47 us beside the other lane).
+constexpr int DT_R = 32, DT_H = 32, DT_RT = DT_R * DT_H / 256;  // rows per thread (4)
+__global__ __launch_bounds__(256) void dec_hidden_kernel(const float* __restrict__ X, int Q, int64_t xm,
+                                                         const float* __restrict__ w1t, const float* __restrict__ b1,
+                                                         int Fh, const float* __restrict__ w2, int n_out,
+                                                         float* __restrict__ part, int E) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* xs = sm;                  // [DT_R][E]
+  float* ws = xs + DT_R * E;       // [E][DT_H]
+  float* hs = ws + E * DT_H;       // [DT_R][DT_H + 1]
+  const int m = blockIdx.z, q0 = blockIdx.x * DT_R, h0 = blockIdx.y * DT_H, tid = threadIdx.x;
+  X += m * xm;
+  part += (int64_t)m * gridDim.y * Q * n_out;
+  const int hw = min(DT_H, Fh - h0);  // hidden units of this tile (the last may be partial)
+  for (int i = tid; i < DT_R * E; i += 256) {
     const int r = i / E;
     xs[i] = q0 + r < Q ? X[(int64_t)(q0 + r) * E + (i - r * E)] : 0.f;
   }
-  __syncthreads();
-  const int kq = tid >> 8, kw = E / DEC_KQ, kb = kq * kw;
-  for (int o = tid & 255; o < Fh; o += 256) {
-    float a[DEC_R];
-#pragma unroll
-    for (int r = 0; r < DEC_R; ++r) a[r] = 0.f;
-    int k = 0;
-    for (; k + 16 <= kw; k += 16) {
-      float w[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) w[j] = w1t[(int64_t)(kb + k + j) * Fh + o];
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-#pragma unroll
-        for (int r = 0; r < DEC_R; ++r) a[r] = fmaf(xs[r * E + kb + k + j], w[j], a[r]);
-    }
-    for (; k < kw; ++k) {
-      const float w = w1t[(int64_t)(kb + k) * Fh + o];
-#pragma unroll
-      for (int r = 0; r < DEC_R; ++r) a[r] = fmaf(xs[r * E + kb + k], w, a[r]);
-    }
-#pragma unroll
-    for (int r = 0; r < DEC_R; ++r) part[(kq * DEC_R + r) * Fh + o] = a[r];
+  for (int i = tid; i < E * DT_H; i += 256) {
+    const int e = i / DT_H;
+    const int cc = i - e * DT_H;
+    ws[i] = cc < hw ? w1t[(int64_t)e * Fh + h0 + cc] : 0.f;
   }
   __syncthreads();
-  for (int i = tid; i < DEC_R * Fh; i += blockDim.x) {
-    const int o = i % Fh;
-    float a = part[i];
+  const int c = tid & (DT_H - 1), rb = (tid / DT_H) * DT_RT;  // DT_RT rows per thread
+  float acc[DT_RT];
 #pragma unroll
-    for (int j = 1; j < DEC_KQ; ++j) a += part[j * DEC_R * Fh + i];
-    hs[i] = gelu_erf(a + b1[o]);  // element i is read and written by this thread only
+  for (int r = 0; r < DT_RT; ++r) acc[r] = 0.f;
+  for (int e = 0; e < E; e += 4) {  // E % 4 == 0: 16-B row reads
+    float w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = ws[(e + i) * DT_H + c];
+#pragma unroll
+    for (int r = 0; r < DT_RT; ++r) {
+      const f32x4 xv = *(const f32x4*)(xs + (rb + r) * E + e);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[r] = fmaf(xv[i], w[i], acc[r]);
+    }
   }
+  const float bb = c < hw ? b1[h0 + c] : 0.f;
+#pragma unroll
+  for (int r = 0; r < DT_RT; ++r) hs[(rb + r) * (DT_H + 1) + c] = c < hw ? gelu_erf(acc[r] + bb) : 0.f;
   __syncthreads();
-  const int wave = tid >> 6, lane = tid & 63;
-  for (int j = wave; j < DEC_R * n_out; j += blockDim.x / 64) {
-    const int r = j / n_out, o = j - r * n_out;
+  for (int pr = tid; pr < DT_R * n_out; pr += 256) {
+    const int r = pr / n_out, j = pr - r * n_out;
     if (q0 + r >= Q) continue;
-    const float* wr = w2 + (int64_t)o * Fh;
+    const float* wr = w2 + (int64_t)j * Fh + h0;
     float a = 0.f;
-    for (int k = lane; k < Fh; k += 64) a = fmaf(hs[r * Fh + k], wr[k], a);
-    a = wave_sum(a);
-    if (lane == 0) out[(int64_t)(q0 + r) * n_out + o] = a + b2[o];
+    for (int k = 0; k < hw; ++k) a = fmaf(hs[r * (DT_H + 1) + k], wr[k], a);
+    part[((int64_t)blockIdx.y * Q + q0 + r) * n_out + j] = a;
   }
+}
+
+__global__ __launch_bounds__(256) void dec_sum_kernel(const float* __restrict__ part, int M, int Q, int nt, int n_out,
+                                                      const float* __restrict__ b2, float* __restrict__ out,
+                                                      int64_t om) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, per = (int64_t)Q * n_out;
+  if (i >= M * per) return;
+  const int64_t m = i / per, k = i - m * per;
+  const float* pm = part + m * nt * per;
+  float a = b2[k % n_out];
+  for (int t = 0; t < nt; ++t) a += pm[t * per + k];
+  out[m * om + k] = a;
 }
 
 // ensemble aggregation (classifier.py:541-566): per query row, per member
@@ -466,13 +469,18 @@ hipError_t launch_add_tokens(const float* tok, int S, int C, const float* posemb
 }
 
 hipError_t launch_decoder(const float* X, int Q, const float* w1t, const float* b1, int Fh, const float* w2,
-                          const float* b2, int n_out, float* out, int E, hipStream_t st) {
-  if (Q <= 0) return hipSuccess;
-  if (E % DEC_KQ) return hipErrorInvalidValue;
-  const size_t lds = (size_t)DEC_R * (E + DEC_KQ * Fh) * sizeof(float);  // 52 KB at E=192, Fh=768
+                          const float* b2, int n_out, float* out, int E, hipStream_t st, int M, int64_t xm, int64_t om,
+                          float* scratch) {
+  if (Q <= 0 || M <= 0) return hipSuccess;
+  if (Fh <= 0 || !scratch || E % 4 != 0) return hipErrorInvalidValue;
+  const size_t lds = (size_t)(DT_R * E + E * DT_H + DT_R * (DT_H + 1)) * sizeof(float);  // 81 KB at E = 192
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(decoder_kernel, dim3((Q + DEC_R - 1) / DEC_R), dim3(1024), lds, st, X, Q, w1t, b1, Fh, w2, b2,
-                     n_out, out, E);
+  const int nt = (Fh + DT_H - 1) / DT_H;
+  hipLaunchKernelGGL(dec_hidden_kernel, dim3((Q + DT_R - 1) / DT_R, nt, M), dim3(256), lds, st, X, Q, xm, w1t, b1, Fh,
+                     w2, n_out, scratch, E);
+  const int64_t n = (int64_t)M * Q * n_out;
+  hipLaunchKernelGGL(dec_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, scratch, M, Q, nt, n_out, b2,
+                     out, om);
   return hipGetLastError();
 }
 

@@ -140,8 +140,10 @@ hipError_t launch_pos_emb(const float* rnd /*[n][E/4]*/, int n, const float* w /
                           const float* b, float* out /*[n][E]*/, int E, hipStream_t st);
 hipError_t launch_add_tokens(const float* tok /*[S][C][E]*/, int S, int C, const float* posemb /*[C][E]*/,
                              float* X /*[C][S][E] slice*/, int E, int* flag, hipStream_t st);
+// M members' decoders: X + m*xm [Q][E] -> out + m*om [Q][n_out]; scratch >= M*(Fh/64)*Q*n_out floats
 hipError_t launch_decoder(const float* X /*[Q][E]*/, int Q, const float* w1t /*[E][Fh]*/, const float* b1, int Fh,
-                          const float* w2, const float* b2, int n_out, float* out, int E, hipStream_t st);
+                          const float* w2, const float* b2, int n_out, float* out, int E, hipStream_t st, int M,
+                          int64_t xm, int64_t om, float* scratch);
 
 hipError_t launch_aggregate(const float* logits /*[M][Q][n_out]*/, int M, int Q, int n_out,
                             const int* perms /*[M][n_cls] or null*/, int n_cls, float temp, int avg_before,
