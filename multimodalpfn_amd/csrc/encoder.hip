@@ -68,8 +68,10 @@ __device__ Moments nan_moments(int n, Fn f, double* red) {
 // 1024 threads (16 waves): each pass over the rows is two strided loads per thread, so the
 // ~9 dependent passes per column are short; reduction slots of 16 waves at red + {0,16,32}
 __global__ __launch_bounds__(1024) void enc_x_stats_kernel(const float* __restrict__ x, int S, int F, int N, int fpg,
-                                                           int nf, float sigma, SlotParams* __restrict__ slots) {
+                                                           int nf, float sigma, SlotParams* __restrict__ slots,
+                                                           int col_lds) {
   __shared__ double red[48];
+  extern __shared__ float colv[];  // col_lds: the slot's column (S rows) staged once for the ~9 passes
   __shared__ int s_cnt[8];
   const int g = blockIdx.x;
   // 1. constancy over all rows (RemoveEmptyFeatures) for each column of the group
@@ -103,8 +105,12 @@ __global__ __launch_bounds__(1024) void enc_x_stats_kernel(const float* __restri
     p.mean = 0.f;
     p.sd = 1.f;
     p.scale = 1.f;
+    if (c >= 0 && col_lds) {
+      for (int s = threadIdx.x; s < S; s += blockDim.x) colv[s] = x[(int64_t)s * F + c];
+      __syncthreads();
+    }
     if (c >= 0) {
-      auto raw = [&](int s) { return x[(int64_t)s * F + c]; };
+      auto raw = [&](int s) { return col_lds ? colv[s] : x[(int64_t)s * F + c]; };
       // NaN handling: torch.nanmean over train rows (inf included)
       {
         double sum = 0.0, cnt = 0.0;
@@ -435,8 +441,11 @@ hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, 
                            hipStream_t st, bool stats) {
   if (G <= 0) return hipSuccess;
   if (fpg > 8 || nf > 8 || nf < fpg) return hipErrorInvalidValue;
-  if (stats)
-    hipLaunchKernelGGL(enc_x_stats_kernel, dim3(G, fpg), dim3(1024), 0, st, x, S, F, N, fpg, nf, sigma, slots);
+  if (stats) {
+    const int col_lds = (size_t)S * sizeof(float) <= 48 * 1024 ? 1 : 0;  // stage the column when it fits
+    hipLaunchKernelGGL(enc_x_stats_kernel, dim3(G, fpg), dim3(1024), col_lds ? (size_t)S * sizeof(float) : 0, st, x, S,
+                       F, N, fpg, nf, sigma, slots, col_lds);
+  }
   if (fpg > 8 || nf > 8 || E > EMB_EMAX || E % 4 != 0 || (int64_t)S * G >= INT32_MAX) return hipErrorInvalidValue;
   const int64_t nblk = ((int64_t)S * G + EMB_TOK - 1) / EMB_TOK;
   hipLaunchKernelGGL(enc_x_embed_kernel, dim3((unsigned)nblk), dim3(256), 0, st, x, S, F, G, fpg, nf, slots, w_enc,
