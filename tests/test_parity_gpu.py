@@ -362,3 +362,27 @@ def test_train_kv_cache_equals_full_forward(prec):
         cache.free()
     assert torch.equal(a, full)
     assert torch.equal(b, full[:37])
+
+
+@pytest.mark.parametrize("mixer,mgm,cap,S", [("MGM+CAP", 64, 24, 300), ("MGM+CAP", 8, 4, 777), ("MGM", 16, 2, 513)])
+def test_mixer_bf16_matches_fp32(mixer, mgm, cap, S):
+    """bf16 mixer path (large-tile DMA-ring GLU GEMM for the MGM head bank, fused k_norm + K|V
+    projection, CAP attention on bf16 keys) against the fp32 parity path on the same weights and
+    image rows, row counts that leave partial 256-row tiles; bf16 tolerance 3e-2 relative."""
+    from synth import synth_image, synth_state_dict
+
+    from multimodalpfn_amd import _lib
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    cfg = ModelConfig(nlayers=1, mixer_type=mixer, mgm_heads=mgm, cap_heads=cap)
+    sd = synth_state_dict(state_dict_spec(cfg), 9)
+    eng = make_model(cfg, sd).engine()
+    im = torch.from_numpy(synth_image(S, 1, 9)).cuda()
+    with torch.inference_mode():
+        ref = eng.mixer_tokens(im, _lib.PREC_F32)
+        got = eng.mixer_tokens(im, _lib.PREC_BF16)
+        eng.status()
+    assert got.shape == ref.shape
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+    assert err < 3e-2, err
