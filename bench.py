@@ -132,14 +132,12 @@ def live_roofline(lib, ctx, T_launch):
     }
 
 
-def time_item_attention(eng, T, reps):
+def time_item_attention(eng, T, reps, S=S_ROWS, N=N_TRAIN):
     """Average launch duration of the sample-axis attention kernel at the workload's shape.
 
     One launch = the whole attention-between-items of one layer (train rows on their own
     heads + test rows of all heads on head 0's K/V), HIP events on the engine stream."""
-    from multimodalpfn_amd import _lib
-
-    H, d, S, N = 6, 32, S_ROWS, N_TRAIN
+    H, d = 6, 32
     Q = S - N
     Npad = (N + 63) // 64 * 64
     dev = eng.device
@@ -168,7 +166,7 @@ def time_item_attention(eng, T, reps):
     ms = e0.elapsed_time(e1) / reps
     flops = 4.0 * T * (N + Q) * N * H * d  # train 4*T*N*N*E + test (MQA) 4*T*Q*N*E
     achieved = flops / (ms * 1e-3) / 1e12
-    traffic, src = attn_traffic(T)
+    traffic, src = attn_traffic(T) if (S, N) == (S_ROWS, N_TRAIN) else (None, None)
     return {
         "bound": "mfma",
         "achieved": round(achieved, 1),
@@ -388,6 +386,13 @@ def main():
         if live is not None and live["token_columns_per_launch"] != T:  # the step's launch shape, alone
             isb = time_item_attention(eng, live["token_columns_per_launch"], args.attn_reps)
             roof["isolated_same_shape_launch"] = {k: isb[k] for k in ("achieved", "frac", "per_launch_ms", "traffic")}
+        # the same kernel at BASELINE.json's other single-GPU shapes (one layer's launch, alone):
+        # B = 4096 support x 100 features (G = 50, T = 51), E = 10k support rows (G = 10, T = 11)
+        roof["other_configs_isolated_launch"] = {}
+        for name, (Tc, Sc, Nc) in {"B: S=5120 N=4096 T=51": (51, 5120, 4096),
+                                   "E: S=12000 N=10000 T=11": (11, 12000, 10000)}.items():
+            r = time_item_attention(eng, Tc, max(3, args.attn_reps // 4), Sc, Nc)
+            roof["other_configs_isolated_launch"][name] = {k: r[k] for k in ("achieved", "frac", "per_launch_ms")}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sd, x, y, image)

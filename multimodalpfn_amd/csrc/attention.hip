@@ -370,6 +370,9 @@ constexpr int A2_NW = 4;
 #ifndef A2_NCH
 #define A2_NCH 2  // 32-query MFMA chains per wave
 #endif
+#ifndef A2_SPT
+#define A2_SPT 1  // 64-key tiles per LDS stage (one barrier per stage)
+#endif
 constexpr int A2_QPW = 32 * A2_NCH;  // queries per wave
 constexpr int A2_QPB = A2_NW * A2_QPW;
 
@@ -425,7 +428,7 @@ __device__ __attribute__((noinline)) void a1_exact_rows(const Attn2Args& p, cons
 #define A2_OCC (A2_NCH == 2 ? 2 : 3)  // waves per SIMD the register budget targets
 #endif
 __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args p) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2][2 * 4096];
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * A2_SPT][2 * 4096];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
 
@@ -441,6 +444,9 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     while (g + 1 < p.H && p.tstart[g + 1] <= rem) ++g;
     chunk = rem - p.tstart[g];
   }
+#ifdef A2_SPRIO  // experiment: static priority for half of the blocks (the later-dispatched CU slots)
+  if ((blockIdx.x >> A2_SPRIO) & 1) __builtin_amdgcn_s_setprio(1);
+#endif
   const int cnt = p.na + (g == p.kvb ? p.H * p.nb : 0);
   const int jw = chunk * A2_QPB + wave * A2_QPW;  // first query of this wave
   const bool active = jw < cnt;               // wave-uniform
@@ -474,28 +480,32 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     }
   }
 
+  const int ntiles = (p.nk + A2_KT - 1) / A2_KT;
+  const bool partial = (p.nk % A2_KT) != 0;
+
   // ---- staging: one 16-B K chunk and one 16-B V^T chunk per thread and tile
   const int krow = tid >> 2, kc = tid & 3;      // K tile [64][32]: row, chunk
   const int vd = tid >> 3, vc = tid & 7;        // V^T tile [32][64]: row d, natural 8-key chunk
-  u32x4 rk, rv;
-  auto gload = [&](int k0, bool mask) {
-    rk = *(const u32x4*)(Kg + (int64_t)(k0 + krow) * 32 + kc * 8);
-    rv = *(const u32x4*)(Vg + (int64_t)vd * p.Npad + k0 + vc * 8);
-    if (mask) {  // keys >= nk: V = 0 so that p = 0 never meets NaN / inf padding
-      bf16x8 e = __builtin_bit_cast(bf16x8, rv);
+  u32x4 rk[A2_SPT], rv[A2_SPT];
+  auto gload = [&](int u, int t) {  // tile t into staging registers u
+    const int k0 = t * A2_KT;
+    rk[u] = *(const u32x4*)(Kg + (int64_t)(k0 + krow) * 32 + kc * 8);
+    rv[u] = *(const u32x4*)(Vg + (int64_t)vd * p.Npad + k0 + vc * 8);
+    if (partial && t == ntiles - 1) {  // keys >= nk: V = 0 so that p = 0 never meets NaN / inf padding
+      bf16x8 e = __builtin_bit_cast(bf16x8, rv[u]);
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (k0 + vc * 8 + j >= p.nk) e[j] = (bf16)0.0f;
-      rv = __builtin_bit_cast(u32x4, e);
+      rv[u] = __builtin_bit_cast(u32x4, e);
     }
   };
   const int koff_w = a2_koff(krow, kc);
   const int voff_w0 = a2_voff(vd, vc & ~1) + 8 * (vc & 1), voff_w1 = a2_voff(vd, vc | 1) + 8 * (vc & 1);
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int u, int buf) {
     unsigned char* Ks = lds[buf];
-    *(u32x4*)(Ks + koff_w) = rk;
-    *(u32x2*)(Ks + 4096 + voff_w0) = u32x2{rv.x, rv.y};
-    *(u32x2*)(Ks + 4096 + voff_w1) = u32x2{rv.z, rv.w};
+    *(u32x4*)(Ks + koff_w) = rk[u];
+    *(u32x2*)(Ks + 4096 + voff_w0) = u32x2{rv[u].x, rv[u].y};
+    *(u32x2*)(Ks + 4096 + voff_w1) = u32x2{rv[u].z, rv[u].w};
   };
   // fragment read offsets (bytes inside a stage)
   int kro[2][2], vro[2][2];
@@ -526,19 +536,16 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  const int ntiles = (p.nk + A2_KT - 1) / A2_KT;
-  const bool partial = (p.nk % A2_KT) != 0;
-
   auto tile = [&](int it, auto maskc, auto firstc) {
     constexpr bool MASK = decltype(maskc)::value;
     constexpr bool FIRST = decltype(firstc)::value;
     const int k0 = it * A2_KT;
-#ifndef A2_NOSTAGE
-    if (it + 1 < ntiles) gload(k0 + A2_KT, partial && it + 2 == ntiles);
-    const unsigned char* Ks = lds[it & 1];
-#else
-    const unsigned char* Ks = lds[0];
-#endif
+    const int sub = it % A2_SPT;  // position inside the stage of A2_SPT tiles
+    if (sub == 0)
+#pragma unroll
+      for (int u = 0; u < A2_SPT; ++u)
+        if (it + A2_SPT + u < ntiles) gload(u, it + A2_SPT + u);
+    const unsigned char* Ks = lds[it % (2 * A2_SPT)];
     if (active) {
       bf16x8 kf[2][2], vf[2][2];
 #pragma unroll
@@ -612,16 +619,20 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 #endif
           }
     }
-#ifndef A2_NOSTAGE
-    if (it + 1 < ntiles) lstore((it + 1) & 1);
-#endif
-#ifndef A2_NOSYNC
-    __syncthreads();
-#endif
+    if (sub == A2_SPT - 1) {  // end of a stage: the next stage's tiles go to the other half of the ring
+#pragma unroll
+      for (int u = 0; u < A2_SPT; ++u)
+        if (it + 1 + u < ntiles) lstore(u, (it + 1 + u) % (2 * A2_SPT));
+      __syncthreads();
+    }
   };
 
-  gload(0, ntiles == 1 && partial);
-  lstore(0);
+#pragma unroll
+  for (int u = 0; u < A2_SPT; ++u)
+    if (u < ntiles) gload(u, u);
+#pragma unroll
+  for (int u = 0; u < A2_SPT; ++u)
+    if (u < ntiles) lstore(u, u);
   __syncthreads();
   if (ntiles == 1) {
     if (partial) tile(0, std::true_type{}, std::true_type{});
