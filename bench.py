@@ -89,7 +89,7 @@ def build_workload(device, world, members_per_gpu):
 
 def attn_traffic(T):
     """HBM bytes per attention launch over T token columns, from the committed PMC pass
-    (tools_attn_pmc.sh: rocprofv3 FETCH_SIZE and WRITE_SIZE runs at that launch shape)."""
+    (tools/attn_pmc.sh: rocprofv3 FETCH_SIZE and WRITE_SIZE runs at that launch shape)."""
     H, d, S, N = 6, 32, S_ROWS, N_TRAIN
     for pmc in sorted((ROOT / "profiles" / "r01").glob("attn_item2_pmc*.json")):
         rec = json.loads(pmc.read_text())

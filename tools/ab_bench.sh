@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B bench of library variants in one GPU call (interleaved, 2 rounds): tools_ab_bench.sh name ...
+# A/B bench of library variants in one GPU call (interleaved, 2 rounds): tools/ab_bench.sh name ...
 # ("default" = the in-tree libmmpfn_hip.so).  Prints value per run.
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 """Per-block timeline of attn_item2_kernel from a -DA2_STAMPS build (diagnostics only).
-Usage: MMPFN_LIB=multimodalpfn_amd/libmmpfn_var_st.so python3 tools_attn_stamps.py"""
+Usage: MMPFN_LIB=multimodalpfn_amd/libmmpfn_var_st.so python3 tools/attn_stamps.py"""
 import ctypes
 import os
 import sys
@@ -8,7 +8,7 @@ from pathlib import Path
 import numpy as np
 import torch
 
-sys.path.insert(0, str(Path(__file__).resolve().parent))
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 from multimodalpfn_amd import _lib  # noqa: E402
 
 T, H, d, S, N = 36, 6, 32, 2298, 1838

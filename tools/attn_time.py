@@ -1,6 +1,6 @@
 """Time the sample-axis attention layer kernel (mmpfn_item_attention_layer) of the library
 named by MMPFN_LIB at the config-C shape and check it against a torch fp32 reference on the GPU.
-Usage: MMPFN_LIB=path python3 tools_attn_time.py [reps]"""
+Usage: MMPFN_LIB=path python3 tools/attn_time.py [reps]"""
 import math
 import os
 import sys
@@ -8,7 +8,7 @@ from pathlib import Path
 
 import torch
 
-sys.path.insert(0, str(Path(__file__).resolve().parent))
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 from multimodalpfn_amd import _lib  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50

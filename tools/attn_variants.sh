@@ -1,6 +1,6 @@
 #!/bin/bash
-# Build attention variants (local, CPU): tools_attn_variants.sh build "name:-DFLAGS" ...
-# Time them (GPU box):                  tools_attn_variants.sh run name ...
+# Build attention variants (local, CPU): tools/attn_variants.sh build "name:-DFLAGS" ...
+# Time them (GPU box):                  tools/attn_variants.sh run name ...
 set -o pipefail
 C=multimodalpfn_amd/csrc
 if [ "$1" = build ]; then
@@ -17,6 +17,6 @@ else
   shift
   mkdir -p gpurun_out
   for name in "$@"; do
-    MMPFN_LIB=multimodalpfn_amd/libmmpfn_var_$name.so timeout -k 10 120 python3 tools_attn_time.py 50 || exit 1
+    MMPFN_LIB=multimodalpfn_amd/libmmpfn_var_$name.so timeout -k 10 120 python3 tools/attn_time.py 50 || exit 1
   done
 fi

@@ -10,7 +10,7 @@ timeout -k 10 120 rocprofv3 -L > $R/gpurun_out/pmc_list.txt 2>&1 || true
 run() {  # name counters...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" -d $R/gpurun_out/pmc_$name -o run --output-format csv -- \
-    python3 $R/tools_prof_forward.py 2 > $R/gpurun_out/pmc_$name.log 2>&1
+    python3 $R/tools/prof_forward.py 2 > $R/gpurun_out/pmc_$name.log 2>&1
 }
 run fetch FETCH_SIZE &&
 run write WRITE_SIZE &&

@@ -1,7 +1,7 @@
 """Profiling driver: a few bf16 member forwards at the config-C shape (for rocprofv3 --pmc passes).
 
 Usage (on the GPU box):  rocprofv3 --pmc <counters> -d <dir> -o run --output-format csv -- \
-                              python3 tools_prof_forward.py [n_forwards]
+                              python3 tools/prof_forward.py [n_forwards]
 """
 
 import os
@@ -11,7 +11,7 @@ from pathlib import Path
 import numpy as np
 import torch
 
-ROOT = Path(__file__).resolve().parent
+ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests" / "golden"))
 

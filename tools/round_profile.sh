@@ -7,4 +7,4 @@ timeout -k 10 600 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.e
 cd /tmp || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/rprof -o run --output-format csv -- \
   python3 $R/bench.py --no-cpu-baseline > $R/gpurun_out/bench_prof.json 2> $R/gpurun_out/bench_prof.err || exit 1
-cd $R && python3 tools_ktrace_grid.py gpurun_out/rprof/run_kernel_trace.csv 40 > gpurun_out/rprof_by_grid.txt
+cd $R && python3 tools/ktrace_grid.py gpurun_out/rprof/run_kernel_trace.csv 40 > gpurun_out/rprof_by_grid.txt

@@ -1,6 +1,6 @@
 """Diagnostics: per-phase cycle stamps of one feat_block_kernel block (needs `make -C multimodalpfn_amd/csrc dbg`).
 
-Run on the GPU box:  MMPFN_LIB=multimodalpfn_amd/libmmpfn_hip_dbg.so python tools_stamps.py
+Run on the GPU box:  MMPFN_LIB=multimodalpfn_amd/libmmpfn_hip_dbg.so python tools/stamps.py
 """
 
 import ctypes
@@ -8,7 +8,7 @@ import os
 import subprocess
 import sys
 
-os.environ.setdefault("MMPFN_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+os.environ.setdefault("MMPFN_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                 "multimodalpfn_amd", "libmmpfn_hip_dbg.so"))
 import tools_prof_forward  # noqa: E402
 

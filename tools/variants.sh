@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel A/B variants.
-#   build (CPU):  SRC=featrow tools_variants.sh build "name:-DFLAGS" ...   -> multimodalpfn_amd/libmmpfn_var_<name>.so
-#   prof (GPU):   tools_variants.sh prof name ...   kernel stats of a 2-member bf16 forward per variant
+#   build (CPU):  SRC=featrow tools/variants.sh build "name:-DFLAGS" ...   -> multimodalpfn_amd/libmmpfn_var_<name>.so
+#   prof (GPU):   tools/variants.sh prof name ...   kernel stats of a 2-member bf16 forward per variant
 set -o pipefail
 C=multimodalpfn_amd/csrc
 if [ "$1" = build ]; then
@@ -20,7 +20,7 @@ else
   R=$PWD; mkdir -p gpurun_out; export TMPDIR=/tmp
   for name in "$@"; do
     cd /tmp && MMPFN_LIB=$R/multimodalpfn_amd/libmmpfn_var_$name.so timeout -k 10 200 rocprofv3 --kernel-trace --stats \
-      -d $R/gpurun_out/var_$name -o run --output-format csv -- python3 $R/tools_prof_forward.py 2 > $R/gpurun_out/var_$name.log 2>&1 || exit 1
-    cd $R && echo "== $name" && python3 tools_kstats.py gpurun_out/var_$name/run_kernel_stats.csv 5
+      -d $R/gpurun_out/var_$name -o run --output-format csv -- python3 $R/tools/prof_forward.py 2 > $R/gpurun_out/var_$name.log 2>&1 || exit 1
+    cd $R && echo "== $name" && python3 tools/kstats.py gpurun_out/var_$name/run_kernel_stats.csv 5
   done
 fi
