@@ -60,6 +60,9 @@ struct mmpfn_cache {
 struct mmpfn_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // every stream bound since the last mmpfn_status: lanes run on their own streams and the NaN
+  // flags they set must be read behind all of them
+  std::vector<hipStream_t> seen_streams;
   std::string err;
   bool have_model = false, finalized = false;
   mmpfn_model_desc d{};
@@ -121,6 +124,12 @@ int fail(mmpfn_ctx* c, int code, const std::string& msg) {
     if (e_ != hipSuccess) return fail(ctx, MMPFN_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+#define RC_(expr)                    \
+  do {                               \
+    int rc_ = (expr);                \
+    if (rc_ != MMPFN_OK) return rc_; \
+  } while (0)
+
 int ensure(mmpfn_ctx* ctx, DevBuf& b, size_t bytes) {
   if (b.bytes >= bytes && b.p) return MMPFN_OK;
   if (b.p) HIPCHK(hipFree(b.p));
@@ -129,6 +138,16 @@ int ensure(mmpfn_ctx* ctx, DevBuf& b, size_t bytes) {
   bytes = (bytes + 255) & ~size_t(255);
   HIPCHK(hipMalloc(&b.p, bytes));
   b.bytes = bytes;
+  return MMPFN_OK;
+}
+
+// the lane's NaN flag: zeroed once when allocated, then only ORed into by the encoder kernels and
+// cleared by mmpfn_status after it has been read, so a NaN in ANY forward queued on the lane since
+// the last status check is reported (not only the last forward's)
+int ensure_flag(mmpfn_ctx* ctx, DevBuf& b, hipStream_t st) {
+  if (b.p) return MMPFN_OK;
+  RC_(ensure(ctx, b, 256));
+  HIPCHK(hipMemsetAsync(b.p, 0, 256, st));
   return MMPFN_OK;
 }
 
@@ -475,9 +494,8 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
     RC(ensure(ctx, ctx->ws_pe, (size_t)(G + C + 1) * E * 4));
     RC(ensure(ctx, ctx->ws_slots, (size_t)(G + 1) * fpg * sizeof(SlotParams)));
     RC(ensure(ctx, ctx->ws_scr, 256));
-    RC(ensure(ctx, ctx->ws_flag, 256));
+    RC(ensure_flag(ctx, ctx->ws_flag, st));
     flag = (int*)ctx->ws_flag.p;
-    HIPCHK(hipMemsetAsync(flag, 0, 4, st));
     HIPCHK(launch_pos_emb(pos_rand, G + C, (const float*)ctx->pe_w.p, (const float*)ctx->pe_b.p,
                           (float*)ctx->ws_pe.p, E, st));
   } else {
@@ -517,9 +535,8 @@ int embed_cached(mmpfn_ctx* ctx, const mmpfn_cache* cc, const float* x, int S, i
   RC(ensure(ctx, ctx->ws_O, R * E * 4));
   const size_t Tpad = (T + 63) / 64 * 64;
   RC(ensure(ctx, ctx->ws_big, (R * E + (size_t)2 * S * Tpad * E) * 4));
-  RC(ensure(ctx, ctx->ws_flag, 256));
+  RC(ensure_flag(ctx, ctx->ws_flag, st));
   int* flag = (int*)ctx->ws_flag.p;
-  HIPCHK(hipMemsetAsync(flag, 0, 4, st));
   float* X = (float*)ctx->ws_X.p;
   const float* pe = (const float*)cc->pe.p;
   if (G)
@@ -816,6 +833,7 @@ mmpfn_ctx* mmpfn_create(int device, void* stream) {
   mmpfn_ctx* c = new mmpfn_ctx();
   c->device = device;
   c->stream = (hipStream_t)stream;
+  c->seen_streams.push_back(c->stream);
   return c;
 }
 
@@ -866,6 +884,9 @@ const char* mmpfn_last_error(const mmpfn_ctx* ctx) { return ctx ? ctx->err.c_str
 int mmpfn_set_stream(mmpfn_ctx* ctx, void* stream) {
   if (!ctx) return MMPFN_ERR_INVALID;
   ctx->stream = (hipStream_t)stream;
+  bool known = false;
+  for (hipStream_t s : ctx->seen_streams) known |= s == ctx->stream;
+  if (!known) ctx->seen_streams.push_back(ctx->stream);
   return MMPFN_OK;
 }
 
@@ -992,16 +1013,23 @@ int mmpfn_aggregate(mmpfn_ctx* ctx, const float* logits, int M, int Q, int n_out
 int mmpfn_status(mmpfn_ctx* ctx) {
   if (!ctx) return MMPFN_ERR_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  // wait for every stream a forward may have been queued on (lanes), not only the bound one
+  for (hipStream_t s : ctx->seen_streams) HIPCHK(hipStreamSynchronize(s));
+  ctx->seen_streams.assign(1, ctx->stream);
   std::vector<void*> flags{ctx->ws_flag.p};
   for (size_t i = 0; i < ctx->lanes.size(); ++i)
     if ((int)i != ctx->cur) flags.push_back(ctx->lanes[i].ws_flag.p);
+  int bad = 0;
   for (void* fp : flags) {
     if (!fp) continue;
     int f = 0;
     HIPCHK(hipMemcpy(&f, fp, 4, hipMemcpyDeviceToHost));
-    if (f) return fail(ctx, MMPFN_ERR_NAN, "There should be no NaNs in the encoded x and y (flag " + std::to_string(f) + ")");
+    if (f) {
+      bad |= f;
+      HIPCHK(hipMemset(fp, 0, 4));  // reported once; the next forwards start clean
+    }
   }
+  if (bad) return fail(ctx, MMPFN_ERR_NAN, "There should be no NaNs in the encoded x and y (flag " + std::to_string(bad) + ")");
   return MMPFN_OK;
 }
 

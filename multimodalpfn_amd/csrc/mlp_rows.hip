@@ -227,10 +227,14 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
   // accumulate onto it, so the residual is never written out and read back
   f32x4 h[2][TT];
   hmma(w1s, h);
+  // chunk 0 overwrites W1 slot 0 (with W1(2)) after its MFMAs: every wave of the block must have
+  // finished reading slot 0 above first -- without this barrier a wave that lags a whole chunk
+  // behind (another kernel sharing its SIMD) read half-replaced W1(0) fragments
+  if (nchunks > 2) __syncthreads();
 
   // one chunk: slots W1(c+1) in w1s[(c+1)&1], W2(c) in w2s[c&1]; W1(c+2) -> w1s[c&1] and
   // W2(c+1) -> w2s[(c+1)&1], written after this chunk's reads; both slots were last read in
-  // chunk c-1 (or, for W1(0), right before chunk 0 -- hence the stash after the reads)
+  // chunk c-1 (or, for W1(0), right before chunk 0, behind the barrier after that read)
   auto chunk = [&](int c, auto morec) {
     constexpr bool MORE = decltype(morec)::value;  // a chunk c+1 exists
 #ifndef MLP_NOSTAGE

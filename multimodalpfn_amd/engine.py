@@ -6,7 +6,8 @@ of the forward runs in ``libmmpfn_hip.so``; this module only moves pointers,
 shapes and the few host-side constants the reference also computes on the host:
 
 * the subspace positional-embedding draw ``torch.randn`` from the model's CPU
-  generator (``transformer.py:421-424,925-931``) -- a bit-exact RNG stream;
+  generator (``transformer.py:421-424,925-931``) -- bit-exact with the reference's CPU
+  forward (see ``pos_rand`` for the GPU stream);
 * the sorted unique train labels of the target encoder (``encoders.py:956-958``).
 """
 
@@ -45,12 +46,24 @@ def model_desc(cfg: ModelConfig) -> _lib.ModelDesc:
     return d
 
 
-def pos_rand(cfg: ModelConfig, n_tokens: int) -> torch.Tensor:
-    """``randn((n_tokens, E//4))`` from a fresh CPU generator, seeded like the reference."""
-    gen = torch.Generator(device="cpu")
+POS_RNG = os.environ.get("MMPFN_POS_RNG", "cpu")  # "cpu" (default) or "device"
+
+
+def pos_rand(cfg: ModelConfig, n_tokens: int, device: torch.device | None = None) -> torch.Tensor:
+    """``randn((n_tokens, E//4))`` from a fresh generator seeded like ``_init_rnd`` (transformer.py:421-424).
+
+    The reference draws on the generator of the device its input lives on (:887-892): on a CPU
+    forward that is the CPU Mersenne-Twister stream, which is what the goldens pin, and the engine
+    reproduces it bit for bit.  On a GPU the reference draws from that GPU's Philox generator in the
+    autocast dtype of its embedded input; that stream depends on the device's grid geometry and dtype,
+    so it is not a fixed target.  ``MMPFN_POS_RNG=device`` draws from a generator on ``device`` (fp32)
+    instead -- the reference's GPU behaviour in kind, parity unpinned.
+    """
+    gdev = device if (POS_RNG == "device" and device is not None) else torch.device("cpu")
+    gen = torch.Generator(device=gdev)
     if cfg.model_seed:  # `if self.seed:` (transformer.py:423)
         gen.manual_seed(cfg.model_seed)
-    return torch.randn((n_tokens, cfg.emsize // 4), generator=gen, dtype=torch.float32)
+    return torch.randn((n_tokens, cfg.emsize // 4), generator=gen, dtype=torch.float32, device=gdev)
 
 
 def target_uniques(y_train: np.ndarray) -> np.ndarray:
@@ -63,6 +76,9 @@ def target_uniques(y_train: np.ndarray) -> np.ndarray:
 
 DEFAULT_LANES = int(os.environ.get("MMPFN_LANES", "2"))  # concurrent member lanes of forward_many
 DEFAULT_BATCH = int(os.environ.get("MMPFN_BATCH", "2"))  # members per batched forward of forward_many
+_DEBUG_SYNC = os.environ.get("MMPFN_DEBUG_SYNC") == "1"  # diagnostics: serialise forward_many's units
+_DEBUG_KEEP = os.environ.get("MMPFN_DEBUG_KEEP") == "1"  # diagnostics: keep every prepared input alive
+_KEEP: list = []
 
 
 class HipEngine:
@@ -130,7 +146,7 @@ class HipEngine:
 
     def _pos(self, n: int) -> torch.Tensor:
         if n not in self._pos_cache:
-            self._pos_cache[n] = pos_rand(self.cfg, n).to(self.device)
+            self._pos_cache[n] = pos_rand(self.cfg, n, self.device).to(self.device)
         return self._pos_cache[n]
 
     # ------------------------------------------------------------------ compute
@@ -167,6 +183,8 @@ class HipEngine:
         G = (F + fpg - 1) // fpg if xd is not None else 0
         uniq = torch.from_numpy(target_uniques(y_np)).to(self.device)
         yd = torch.from_numpy(y_np).to(self.device)
+        if _DEBUG_KEEP:
+            _KEEP.append((xd, td, yd, uniq))
         return xd, td, yd, uniq, S, F, C, N, G
 
     def forward(self, x, tokens, y_train, precision: int, check_nan: bool = True) -> torch.Tensor:
@@ -326,6 +344,8 @@ class HipEngine:
                 with torch.cuda.stream(streams[k % lanes]):
                     self._check(self.lib.mmpfn_select_lane(self.ctx, k % lanes), "mmpfn_select_lane")
                     run(u)
+                    if _DEBUG_SYNC:
+                        torch.cuda.synchronize(self.device)
         finally:
             self._check(self.lib.mmpfn_select_lane(self.ctx, 0), "mmpfn_select_lane")
             for st in streams:
@@ -354,8 +374,14 @@ class HipEngine:
         pd = None
         if perms is not None:
             pd = torch.as_tensor(np.asarray(perms, dtype=np.int32).reshape(M, n_classes)).to(self.device)
-        cw = None if class_weights is None else self._dev(class_weights)
         C = n_classes if (temperature != 1 or perms is not None) else n_out
+        cw = None
+        if class_weights is not None:
+            cw = self._dev(class_weights).reshape(-1)
+            if cw.numel() != C:  # the reference's `output * class_prob_in_train` fails on this broadcast too
+                raise RuntimeError(
+                    f"The size of tensor a ({C}) must match the size of tensor b ({cw.numel()}) at non-singleton "
+                    "dimension 1 (balance_probabilities with softmax_temperature == 1 and no class permutation)")
         out = torch.empty((Q, C), device=self.device, dtype=torch.float32)
         self._bind_stream()
         self._check(
@@ -366,6 +392,9 @@ class HipEngine:
         return out
 
     def status(self) -> None:
+        """Wait for every stream the context ran on and raise ``ValueError`` if any forward since the
+        last call saw NaNs in its embedded input (transformer.py:727-731,790-796)."""
+        self._bind_stream()
         self._check(self.lib.mmpfn_status(self.ctx), "mmpfn_forward")
 
     # ------------------------------------------------------------------ parity taps

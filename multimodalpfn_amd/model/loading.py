@@ -8,9 +8,13 @@ the reference passes them.  Differences, both deliberate:
 
 * the file is read with ``torch.load(..., weights_only=True)``: tensors and plain
   containers only, nothing executed from the file;
-* ``strict=False`` in the reference leaves any parameter missing from the file at
-  its (unseeded, random) initialisation.  Nothing can depend on those values, so
-  here a missing parameter is an error naming it.
+* ``strict=False`` (``loading.py:540``): a modality head (``mgm.*`` / ``cap.*`` /
+  ``moe.*``) missing from the file -- a base TabPFN checkpoint that was never
+  fine-tuned with images -- keeps its initialisation, as in the reference.  The
+  reference's init draws from the unseeded global RNG; here it is drawn from
+  ``torch.manual_seed(model_seed)`` with the reference modules' own init rules, so it
+  is reproducible, and a warning names the missing heads.  A missing TRUNK parameter
+  (encoders, layers, decoder) is still an error: no reference checkpoint lacks one.
 """
 
 from __future__ import annotations
@@ -87,14 +91,49 @@ def model_config_from_checkpoint(config: dict, *, model_seed: int, mixer_type: s
     )
 
 
+MIXER_PREFIXES = ("mgm.", "cap.", "moe.")
+
+
+@torch.no_grad()
+def init_mixer_(model: PerFeatureTransformer, seed: int) -> None:
+    """Initialise the modality heads like the reference constructors (transformer.py:33-128):
+    ``nn.Linear`` / ``nn.LayerNorm`` defaults, ``nn.MultiheadAttention._reset_parameters``,
+    CAP queries ``randn * 1e-2`` (:64) -- from ``torch.manual_seed(seed)`` instead of the
+    reference's unseeded global stream."""
+    with torch.random.fork_rng(devices=[]):
+        torch.manual_seed(seed)
+        for name in ("mgm", "moe", "cap"):
+            mod = getattr(model, name, None)
+            if mod is None:
+                continue
+            for m in mod.modules():  # constructor order: the layers first, then the MHA's own reset
+                if isinstance(m, (nn.Linear, nn.LayerNorm)):
+                    m.reset_parameters()
+            for m in mod.modules():
+                if isinstance(m, nn.MultiheadAttention):
+                    m._reset_parameters()  # in_proj xavier, in_proj / out_proj biases zero
+            if name == "cap":
+                mod.queries.copy_(torch.randn(mod.queries.shape) * 1e-2)
+
+
 def build_model(cfg: ModelConfig, state_dict: dict[str, Any]) -> PerFeatureTransformer:
-    """Instantiate the model and load ``state_dict`` (extra keys ignored, missing keys rejected)."""
+    """Instantiate the model and load ``state_dict`` with the reference's ``strict=False``
+    (loading.py:540): extra keys ignored, missing modality-head tensors keep their (seeded)
+    initialisation with a warning, a missing trunk tensor is an error."""
     model = PerFeatureTransformer(cfg)
     names = [n for n, _ in state_dict_spec(cfg)]
     missing = [n for n in names if n not in state_dict]
+    trunk = [n for n in missing if not n.startswith(MIXER_PREFIXES)]
+    if trunk:
+        raise ValueError(f"checkpoint lacks {len(trunk)} trunk parameter(s) the model needs, e.g. {trunk[:5]}")
     if missing:
-        raise ValueError(f"checkpoint lacks {len(missing)} parameter(s) the model needs, e.g. {missing[:5]}")
-    model.load_state_dict({n: torch.as_tensor(state_dict[n]) for n in names}, strict=True)
+        init_mixer_(model, cfg.model_seed)
+        heads = sorted({n.split(".")[0] for n in missing})
+        warnings.warn(f"checkpoint has no weights for the modality head(s) {heads} ({len(missing)} tensors): "
+                      f"they keep their initialisation (seeded by model_seed={cfg.model_seed}), as the "
+                      "reference's strict=False load leaves them", stacklevel=3)
+    model.load_state_dict({n: torch.as_tensor(state_dict[n]) for n in names if n in state_dict}, strict=False)
+    model.cache_trainset_representation = True  # loading.py:497
     model.eval()
     return model
 

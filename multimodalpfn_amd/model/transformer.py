@@ -26,6 +26,7 @@ the fp32 parity mode.
 
 from __future__ import annotations
 
+import copy
 from typing import Any
 
 import torch
@@ -237,6 +238,23 @@ class PerFeatureTransformer(nn.Module):
         self._forced_dtype: torch.dtype | None = None
         self._engines: dict[Any, Any] = {}
         self._weights_version = 0
+        self._train_cache = None  # device train-KV cache of the last train-only forward (fit_with_cache)
+
+    def __deepcopy__(self, memo):
+        """``deepcopy(model)`` (InferenceEngineCacheKV.prepare, inference.py:421): parameters are
+        copied; the packed device weights are shared with the original (same values), the train-KV
+        cache is not (each copy caches its own member)."""
+        cls = self.__class__
+        new = cls.__new__(cls)
+        memo[id(self)] = new
+        for k, v in self.__dict__.items():
+            if k == "_engines":
+                new.__dict__[k] = v  # shared: same weights
+            elif k == "_train_cache":
+                new.__dict__[k] = None
+            else:
+                new.__dict__[k] = copy.deepcopy(v, memo)
+        return new
 
     # ------------------------------------------------------------------ module plumbing
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):  # noqa: D102
@@ -276,9 +294,6 @@ class PerFeatureTransformer(nn.Module):
         for layer in self.transformer_encoder.layers:
             layer.save_peak_mem_factor = factor
 
-    def empty_trainset_representation_cache(self) -> None:
-        """transformer.py:999-1001 (no KV cache kept across calls)."""
-
     # ------------------------------------------------------------------ engine
     def _effective_config(self) -> ModelConfig:
         norm = next(e for e in self.encoder if isinstance(e, InputNormalizationEncoderStep))
@@ -305,7 +320,9 @@ class PerFeatureTransformer(nn.Module):
         """The HIP engine for ``device`` (built lazily, weights uploaded once)."""
         from multimodalpfn_amd.engine import HipEngine
 
-        dev = device or self._device()
+        dev = torch.device(device) if device is not None else self._device()
+        if dev.type == "cuda" and dev.index is None:  # "cuda" and "cuda:<current>" are one engine
+            dev = torch.device("cuda", torch.cuda.current_device())
         cfg = self._effective_config()
         key = (str(dev), cfg.remove_outliers_sigma, cfg.features_per_group, cfg.model_seed)
         eng = self._engines.get(key)
@@ -342,8 +359,6 @@ class PerFeatureTransformer(nn.Module):
         if not kwargs.get("only_return_standard_out", True):
             raise NotImplementedError("only the standard decoder output is served by the engine")
         sep = kwargs.get("single_eval_pos")
-        if not sep:
-            raise ValueError("single_eval_pos (number of train rows) is required")
         dev = self._device()
         eng = self.engine(dev)
         prec = kwargs.get("precision")
@@ -357,8 +372,38 @@ class PerFeatureTransformer(nn.Module):
             tokens = eng.mixer_tokens(img, prec)
         if x is not None and x.dim() == 3:
             x = x[:, 0, :]
+        if not sep:
+            # test rows only against the cached train representation (transformer.py:593-595,779-784;
+            # layer.py:311,391-394): the call form of InferenceEngineCacheKV.iter_outputs
+            # (inference.py:499-507)
+            if not self.cache_trainset_representation:
+                raise ValueError("single_eval_pos (number of train rows) is required")
+            if y is not None:
+                raise ValueError("a cached-trainset call takes no y (transformer.py:593-595)")
+            cache = self._train_cache
+            if cache is None or cache.engine is not eng or not cache.handle:
+                raise RuntimeError(
+                    "single_eval_pos=None needs a train-KV cache: call the model once on the train rows only "
+                    "(single_eval_pos=len(X_train), as InferenceEngineCacheKV.prepare does) with "
+                    "cache_trainset_representation=True")
+            return eng.cache_predict(cache, x, tokens).unsqueeze(1)
         if y.dim() > 1:
             y = y.reshape(-1)
         y = y[:sep]
+        S = x.shape[0] if x is not None else tokens.shape[0]
+        if self.cache_trainset_representation and sep == S:
+            # train rows only (InferenceEngineCacheKV.prepare, inference.py:425-436): keep this
+            # member's head-0 K/V per layer and encoder statistics on the device; the reference
+            # returns the (empty) test-row output
+            if self._train_cache is not None:
+                self._train_cache.free()
+            self._train_cache = eng.cache_build(x, tokens, y, prec)
+            return torch.empty((0, 1, self.cfg.n_out), device=dev, dtype=torch.float32)
         logits = eng.forward(x, tokens, y, prec)
         return logits.unsqueeze(1)
+
+    def empty_trainset_representation_cache(self) -> None:
+        """transformer.py:999-1001: drop the train-KV cache."""
+        if self._train_cache is not None:
+            self._train_cache.free()
+            self._train_cache = None

@@ -2,7 +2,7 @@
 
 Tolerances (north star: fp32 logits within 1e-4 relative, argmax bit-exact):
   fp32 parity mode : max|d logits| <= 1e-4 * max(1, max|ref|), argmax identical
-  bf16 perf mode   : max|d logits| <= 5e-2 * max(1, max|ref|), argmax agreement >= 90 %
+  bf16 perf mode   : max|d logits| <= 2e-2 * max(1, max|ref|) (about 2x the measured worst), argmax >= 95 %
 """
 
 import math
@@ -17,7 +17,7 @@ from oracle.forward import layer_forward, oracle_forward
 pytestmark = pytest.mark.gpu
 
 F32_TOL = 1e-4
-BF16_TOL = 5e-2
+BF16_TOL = 2e-2  # measured 3.1e-3 .. 9.5e-3 over the goldens (profiles/r02/pytest_gpu_r02a.log)
 
 
 def make_model(cfg, sd):
@@ -56,8 +56,9 @@ def test_forward_bf16_close_to_reference(case):
     assert np.isfinite(out).all()
     err = rel_err(out, z["logits"])
     agree = (out.argmax(1) == z["logits"].argmax(1)).mean()
+    print(f"bf16 {case}: rel err {err:.3e}, argmax agreement {agree:.3f}")
     assert err <= BF16_TOL, err
-    assert agree >= 0.9, agree
+    assert agree >= 0.95, agree
 
 
 def test_embedding_and_layer_taps_fp32():
