@@ -6,17 +6,22 @@ heads) + CAP (24 queries) mixer, 12-layer E=192 PerFeatureTransformer, 4 ensembl
 members per GPU (feature-shuffle + class-permutation members as EnsembleConfig
 builds them), synthetic data and random-init weights of that architecture.
 
-One step = one ``predict_proba`` pass of the hot path with inputs resident in HBM:
-mixer once (the image is identical for every member), 4 member forwards per GPU,
-one RCCL all-gather of the per-member logits, ensemble softmax-mean.  ``value`` =
-sum over members of (N + Q) / wall time, aggregated over all ranks (weak scaling:
-4 members per GPU).  Launch with ``torchrun --nproc-per-node N bench.py --gpus N``
-for N > 1.
+One step = one ``predict_proba`` of the hot path on device-resident inputs: mixer once
+(the image is identical for every member), 4 member forwards per GPU, one RCCL
+all-gather of the per-member logits, ensemble softmax-mean.  ``value`` = sum over
+members of (N + Q) / wall time, aggregated over all ranks (weak scaling: 4 members
+per GPU); nothing else runs in the timed region.  Launch with ``torchrun
+--nproc-per-node N bench.py --gpus N`` for N > 1.
 
-Also reported: ``roofline`` of the dominant kernel (sample-axis attention, bf16
-MFMA; algorithmic flops 4*T*Nq*Nk*E per launch; every launch inside the timed region
-bracketed by HIP events on its lane stream, mmpfn_kernel_timing) and ``cpu_baseline`` (the oracle's CPU restatement of the same
-forward -- the reference's torch-SDPA branch -- on the host cores, bounded sample).
+Also reported (each in its own pass, outside the headline's timed region):
+``roofline`` of the dominant kernel (sample-axis attention, bf16 MFMA; algorithmic
+flops 4*T*Nq*Nk*E per launch; every launch of a separate pass of the same steps
+bracketed by HIP events on its lane stream, mmpfn_kernel_timing), ``f32_parity_mode``
+(the same step in the fp32 parity mode), ``config_D`` (image + text, 32 members),
+``api_end_to_end`` (MMPFNClassifier.predict_proba from host numpy, PCIe-inclusive),
+``kv_cache_predict`` (fit_with_cache serving) and ``cpu_baseline`` /
+``cpu_baseline_einsum`` (the oracle's CPU restatement of the same forward in the
+reference's two attention branches, on the host cores, one member).
 """
 
 from __future__ import annotations
@@ -56,27 +61,32 @@ def parse():
     p.add_argument("--batch", type=int, default=None, help="members per batched forward (default: engine's)")
     p.add_argument("--api-steps", type=int, default=3, help="timed predict_proba calls of the API leg (0: skip)")
     p.add_argument("--no-kv-cache", dest="kv_cache", action="store_false", help="skip the fit_with_cache leg")
+    p.add_argument("--no-config-d", dest="config_d", action="store_false", help="skip the config-D leg")
+    p.add_argument("--no-f32", dest="f32_leg", action="store_false", help="skip the fp32 parity-mode leg")
+    p.add_argument("--no-cpu-einsum", dest="cpu_einsum", action="store_false",
+                   help="skip the einsum-branch CPU baseline (the SDPA branch always runs)")
     return p.parse_args()
 
 
-def build_workload(device, world, members_per_gpu):
+def build_workload(device, world, members_per_gpu, n_mod=1, seed=2):
+    """Config C (seed 2, image [S,1,768]) or D (seed 3, image + text [S,2,768]), SURVEY.md 8d."""
     from synth import synth_image, synth_labels, synth_state_dict, synth_table
 
     from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
     from multimodalpfn_amd.model.transformer import PerFeatureTransformer
 
     cfg = ModelConfig(mgm_heads=MGM, cap_heads=CAP)
-    sd = synth_state_dict(state_dict_spec(cfg), 2)
+    sd = synth_state_dict(state_dict_spec(cfg), seed)
     model = PerFeatureTransformer(cfg)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     norm = next(e for e in model.encoder if "InputNormalizationEncoderStep" in str(e.__class__))
     norm.remove_outliers, norm.remove_outliers_sigma = True, 12.0  # classifier.fit (classifier.py:396-406)
     model.to(device)
-    x = synth_table(S_ROWS, N_FEAT, 2, n_cat=N_CAT)
-    y = synth_labels(S_ROWS, N_CLASSES, 2)
-    image = synth_image(S_ROWS, 1, 2)
+    x = synth_table(S_ROWS, N_FEAT, seed, n_cat=N_CAT)
+    y = synth_labels(S_ROWS, N_CLASSES, seed)
+    image = synth_image(S_ROWS, n_mod, seed)
     M = members_per_gpu * world
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(seed - 2)
     members = []
     for m in range(M):
         fperm = rng.permutation(N_FEAT)  # ShuffleFeaturesStep
@@ -236,8 +246,10 @@ def kv_cache_leg(eng, members, img, prec, steps):
     return out
 
 
-def cpu_baseline(sd, x, y, image):
-    """Oracle (CPU restatement of the reference forward, SDPA branch) on one member."""
+def cpu_baseline(sd, x, y, image, use_sdpa=True):
+    """Oracle (CPU restatement of the reference forward) on one member, in the attention branch
+    the reference takes on a GPU box (torch SDPA, multi_head_attention.py:693-717) or its
+    explicit einsum-softmax fallback (:718-729, the branch a CPU-only host takes)."""
     from multimodalpfn_amd.model.spec import ModelConfig
     from oracle.forward import OracleSpec, oracle_forward
 
@@ -248,15 +260,16 @@ def cpu_baseline(sd, x, y, image):
     w = {k: torch.from_numpy(v) for k, v in sd.items()}
     args = (spec, w, torch.from_numpy(x), torch.from_numpy(image), torch.from_numpy(y[:N_TRAIN]))
     t0 = time.perf_counter()
-    oracle_forward(*args, use_sdpa=True)
+    oracle_forward(*args, use_sdpa=use_sdpa)
     dt = time.perf_counter() - t0
+    branch = "torch SDPA branch" if use_sdpa else "einsum-softmax branch"
     return {
         "value": round(S_ROWS / dt, 2),
         "unit": "rows/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"1 member forward of config C (S={S_ROWS}, 12 layers, MGM64+CAP24, fp32, torch SDPA "
-                  f"branch) on {threads} host threads: {dt:.1f} s",
+        "sample": f"1 member forward of config C (S={S_ROWS}, 12 layers, MGM64+CAP24, fp32, {branch}) on "
+                  f"{threads} host threads: {dt:.1f} s",
     }
 
 
@@ -309,6 +322,82 @@ def api_end_to_end(cfg, sd, x, y, image, n_estimators, prec_f32, steps, world):
     }
 
 
+def timed_steps(step, steps, warmup, world, device):
+    """W untimed steps, then K steps bracketed by barrier + synchronize on both sides; the max
+    wall time over ranks (bench contract)."""
+    import torch.distributed as dist
+
+    for _ in range(warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    return dt
+
+
+def make_step(eng, members, mine, assignment, rank, img, prec, lanes, batch):
+    """One predict_proba of the hot path on device-resident inputs (classifier.py:517-576 minus the
+    host-side input validation / per-member transform and the final copy to host): the mixer once,
+    this rank's members through forward_many, one RCCL all-gather of the logits, the ensemble
+    softmax-mean on the device."""
+    from multimodalpfn_amd.parallel import allgather_logits
+
+    perms = np.stack([m[2] for m in members])
+
+    def step():
+        tokens = eng.mixer_tokens(img, prec)
+        outs = eng.forward_many([(members[m][0], tokens, members[m][1]) for m in mine], prec, lanes, batch)
+        allm = allgather_logits(torch.stack(outs), assignment, rank)
+        return eng.aggregate(allm, perms, N_CLASSES, 0.9, False)
+
+    return step
+
+
+def config_d_leg(device, world, rank, args, prec):
+    """BASELINE config D: image + text [S,2,768] (petfinder.py:194 shape), MGM64 + CAP24 (CAP over
+    2 x 64 MGM tokens), 32 members (run.py's no-preprocessing members: feature shuffle + class
+    permutation) sharded over the ranks, one all-gather.  rows/s = 32 * (N + Q) / step time."""
+    from multimodalpfn_amd.parallel import lpt_assign
+
+    members_total = 32
+    per = -(-members_total // world)
+    cfg, sd, model, x, y, image, members = build_workload(device, world, per, n_mod=2, seed=3)
+    members = members[:members_total]
+    eng = model.engine(device)
+    img = torch.from_numpy(image).to(device)
+    T = (N_FEAT + 1) // 2 + CAP + 1
+    assignment = lpt_assign([float(T * S_ROWS * N_TRAIN)] * members_total, world)
+    step = make_step(eng, members, assignment[rank], assignment, rank, img, prec, args.lanes, args.batch)
+    probs = step()
+    eng.status()
+    assert torch.isfinite(probs).all()
+    k = max(3, args.steps // 4)
+    dt = timed_steps(step, k, max(1, args.warmup // 4), world, device)
+    eng.close()
+    return {
+        "value": round(members_total * S_ROWS * k / dt, 1),
+        "unit": "rows/s",
+        "ms_per_step": round(dt / k * 1e3, 3),
+        "steps": k,
+        "members_total": members_total,
+        "members_per_gpu": len(assignment[rank]),
+        "workload": "config D: image + text [S,2,768], MGM 64 + CAP 24 (CAP over 128 MGM tokens), N=1838 + Q=460, "
+                    "F=21, 12 layers, 32 members (feature shuffle + class permutation) sharded over the GPUs, "
+                    "one all-gather of the logits",
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -323,7 +412,7 @@ def main():
         dist.init_process_group("nccl", device_id=device)
 
     from multimodalpfn_amd import _lib
-    from multimodalpfn_amd.parallel import allgather_logits, lpt_assign
+    from multimodalpfn_amd.parallel import lpt_assign
 
     prec = _lib.PREC_BF16 if args.precision == "bf16" else _lib.PREC_F32
     cfg, sd, model, x, y, image, members = build_workload(device, world, args.members)
@@ -333,43 +422,38 @@ def main():
     T = (N_FEAT + 1) // 2 + CAP + 1
     assignment = lpt_assign([float(T * S_ROWS * N_TRAIN)] * M, world)
     mine = assignment[rank]
-    perms = np.stack([members[m][2] for m in range(M)])
-
-    def step():
-        tokens = eng.mixer_tokens(img, prec)
-        outs = eng.forward_many([(members[m][0], tokens, members[m][1]) for m in mine], prec, args.lanes,
-                                args.batch)
-        local = torch.stack(outs)
-        allm = allgather_logits(local, assignment, rank)
-        return eng.aggregate(allm, perms, N_CLASSES, 0.9, False)
+    step = make_step(eng, members, mine, assignment, rank, img, prec, args.lanes, args.batch)
 
     probs = step()
     eng.status()  # NaN check once (reference raises ValueError)
     assert torch.isfinite(probs).all()
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    eng.lib.mmpfn_kernel_timing(eng.ctx, 1)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    eng.lib.mmpfn_kernel_timing(eng.ctx, 0)
-    batch = eng.batch if args.batch is None else args.batch
-    live = live_roofline(eng.lib, eng.ctx, T * min(batch, len(mine))) if rank == 0 else None
-    if world > 1:
-        tt = torch.tensor([dt], device=device, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    # ---- headline: nothing but the steps in the timed region
+    dt = timed_steps(step, args.steps, args.warmup, world, device)
     rows = M * S_ROWS * args.steps
     value = rows / dt
     step_flop = len(mine) * forward_flops(T) + mixer_flops()  # per rank
     wf = step_flop * args.steps / dt / 1e12  # TFLOP/s of one rank (its wall time is the job's max)
+
+    # ---- live roofline of the dominant kernel: a SEPARATE pass of the same steps with every
+    #      attention launch bracketed by HIP events on its lane stream (kept out of the headline)
+    eng.lib.mmpfn_kernel_timing(eng.ctx, 1)
+    dt_live = timed_steps(step, args.steps, 0, world, device)
+    eng.lib.mmpfn_kernel_timing(eng.ctx, 0)
+    batch = eng.batch if args.batch is None else args.batch
+    live = live_roofline(eng.lib, eng.ctx, T * min(batch, len(mine))) if rank == 0 else None
+    if live is not None:
+        live["timing"] += f"; a separate pass of {args.steps} steps ({dt_live / args.steps * 1e3:.3f} ms per step)"
+
+    # ---- the fp32 parity mode (what the 1e-4 logits contract costs)
+    f32 = None
+    if args.f32_leg and prec != _lib.PREC_F32:
+        step32 = make_step(eng, members, mine, assignment, rank, img, _lib.PREC_F32, args.lanes, args.batch)
+        k32 = max(3, args.steps // 6)
+        dt32 = timed_steps(step32, k32, 1, world, device)
+        f32 = {"value": round(M * S_ROWS * k32 / dt32, 1), "unit": "rows/s", "ms_per_step": round(dt32 / k32 * 1e3, 3),
+               "steps": k32, "dtype": "f32",
+               "note": "the same step in the fp32 parity mode (fp32-input MFMA everywhere; logits within 1e-4 "
+                       "of the oracle)"}
 
     api = None
     if args.api_steps > 0:
@@ -393,9 +477,13 @@ def main():
                                    "E: S=12000 N=10000 T=11": (11, 12000, 10000)}.items():
             r = time_item_attention(eng, Tc, max(3, args.attn_reps // 4), Sc, Nc)
             roof["other_configs_isolated_launch"][name] = {k: r[k] for k in ("achieved", "frac", "per_launch_ms")}
-    cpu = None
+    eng.close()
+    cfg_d = config_d_leg(device, world, rank, args, prec) if args.config_d else None
+    cpu = cpu_e = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(sd, x, y, image)
+        cpu = cpu_baseline(sd, x, y, image, use_sdpa=True)
+        if args.cpu_einsum:
+            cpu_e = cpu_baseline(sd, x, y, image, use_sdpa=False)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -413,9 +501,12 @@ def main():
             "config": {
                 "workload": "config C: PAD-UFES-20 image+tabular, N=1838 support + Q=460 query rows, F=21 "
                             "(18 cat + 3 num), image [S,1,768], MGM 64 heads + CAP 24, 12 layers E=192",
+                "step": "predict_proba on device-resident inputs (SURVEY 8d's wall(predict_proba) without the "
+                        "host-side validation / per-member transform and the PCIe copies: those are in "
+                        "api_end_to_end): mixer once, every member's 12-layer forward, all-gather, softmax-mean",
                 "members_per_gpu": args.members,
                 "lanes": eng.lanes if args.lanes is None else args.lanes,
-                "members_per_batched_forward": eng.batch if args.batch is None else args.batch,
+                "members_per_batched_forward": batch,
                 "members_total": M,
                 "rows_per_member": S_ROWS,
                 "tokens_per_row": T,
@@ -430,7 +521,10 @@ def main():
                 "note": "algorithmic flops of the mixer + every member's 12-layer stack (SURVEY.md 8d) / step time",
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_einsum": cpu_e,
             "api_end_to_end": api,
+            "f32_parity_mode": f32,
+            "config_D": cfg_d,
             "kv_cache_predict": kv,
         }
         print(json.dumps(line))

@@ -17,6 +17,7 @@ from oracle.forward import layer_forward, oracle_forward
 pytestmark = pytest.mark.gpu
 
 F32_TOL = 1e-4
+LARGE_BF16_TOL = {"B": 5e-2, "E": 5e-2}
 BF16_TOL = 2e-2  # measured 3.1e-3 .. 9.5e-3 over the goldens (profiles/r02/pytest_gpu_r02a.log)
 
 
@@ -330,8 +331,10 @@ def test_large_config_matches_oracle_on_device(name, S, N, F, n_cls, seed):
     assert np.isfinite(f32).all() and np.isfinite(b16).all()
     assert rel_err(f32, ref) <= F32_TOL, (name, rel_err(f32, ref))
     assert (f32.argmax(1) == ref.argmax(1)).all()
-    assert rel_err(b16, ref) <= BF16_TOL, (name, rel_err(b16, ref))
-    assert (b16.argmax(1) == ref.argmax(1)).mean() >= 0.9
+    eb, agree = rel_err(b16, ref), float((b16.argmax(1) == ref.argmax(1)).mean())
+    print(f"bf16 {name}: rel err {eb:.3e}, argmax agreement {agree:.4f}; fp32 rel err {rel_err(f32, ref):.3e}")
+    assert eb <= LARGE_BF16_TOL[name[0]], (name, eb)
+    assert agree >= 0.95, agree
 
 
 @pytest.mark.parametrize("prec", [0, 1])
