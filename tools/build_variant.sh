@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build the whole engine with extra compile flags into multimodalpfn_amd/libmmpfn_var_<name>.so
+# (local, CPU):  tools/build_variant.sh name "-DFLAG=1 ..."
+set -o pipefail
+name=$1; flags=$2
+C=multimodalpfn_amd/csrc
+B=/tmp/mmpfn_var_$name
+mkdir -p $B
+for src in capi.cpp gemm.hip attention.hip encoder.hip mixer.hip mlp.hip mlp_rows.hip featblock.hip featrow.hip rowgemm.hip; do
+  extra=""; [ $src = attention.hip ] && extra="-fno-honor-nans"
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -mllvm -amdgpu-mfma-vgpr-form=1 \
+    $extra $flags -x hip -c $C/$src -o $B/$src.o &
+done
+wait
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o multimodalpfn_amd/libmmpfn_var_$name.so $B/*.o && echo built $name
