@@ -27,6 +27,11 @@
  *          (:362-372) and test rows against head 0's K/V (:344-358) together
  *   mmpfn_status
  *       <- model/transformer.py:727-731,790-796 NaN checks (ValueError)
+ *   mmpfn_feature_attention / mmpfn_item_attention_block / mmpfn_mlp_ln
+ *       <- model/layer.py:332-339 / :341-379 / :410-424 with the post-norms :437-455
+ *          (one PerFeatureEncoderLayer sublayer each)
+ *   mmpfn_mgm / mmpfn_cap
+ *       <- model/transformer.py:33-57 MultiheadGatedMLP / :60-88 CrossAttentionPooler
  */
 #ifndef MMPFN_HIP_H_
 #define MMPFN_HIP_H_
@@ -179,6 +184,19 @@ void mmpfn_cache_free(mmpfn_ctx* ctx, mmpfn_cache* cache);
  * durations, the launch count and their algorithmic flops (4*T*(N+Q)*N*E each). */
 int mmpfn_kernel_timing(mmpfn_ctx* ctx, int enable);
 int mmpfn_kernel_timing_read(mmpfn_ctx* ctx, double* total_ms, int64_t* launches, double* flops);
+
+/* Per-sublayer taps: one sublayer of layer `layer` on a caller-provided state, in place, on the
+ * context stream (the forward itself fuses across these seams: the bf16 item-attention
+ * out-projection runs inside the MLP kernel there).  X: device [T][S][E] fp32, the engine's
+ * token-major state of ONE member (reference order [S][T][E] transposed).  `rows` = S * T. */
+int mmpfn_feature_attention(mmpfn_ctx* ctx, int layer, float* X, int S, int T, int precision);
+/* train rows [0, N) attend their own heads, rows [N, S) head 0's K/V (MQA) */
+int mmpfn_item_attention_block(mmpfn_ctx* ctx, int layer, float* X, int S, int T, int N, int precision);
+int mmpfn_mlp_ln(mmpfn_ctx* ctx, int layer, float* X, int64_t rows, int precision);
+/* modality heads: image [S][n_mod][nhid] -> MGM tokens [S][mgm*n_mod][E] (head-major, as the
+ * reference concatenates them); MGM tokens [S][M][E] -> CAP tokens [S][cap][E] */
+int mmpfn_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int precision);
+int mmpfn_cap(mmpfn_ctx* ctx, const float* mgm_tokens, int S, int M, float* tokens, int precision);
 
 #ifdef __cplusplus
 }

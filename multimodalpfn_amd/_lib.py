@@ -77,6 +77,11 @@ SIGNATURES = [
     ("mmpfn_cache_bytes", _i64, [_vp]),
     ("mmpfn_cache_free", None, [_vp, _vp]),
     ("mmpfn_kernel_timing", _i, [_vp, _i]),
+    ("mmpfn_feature_attention", _i, [_vp, _i, _vp, _i, _i, _i]),
+    ("mmpfn_item_attention_block", _i, [_vp, _i, _vp, _i, _i, _i, _i]),
+    ("mmpfn_mlp_ln", _i, [_vp, _i, _vp, _i64, _i]),
+    ("mmpfn_mgm", _i, [_vp, _vp, _i, _i, _vp, _i]),
+    ("mmpfn_cap", _i, [_vp, _vp, _i, _i, _vp, _i]),
     ("mmpfn_kernel_timing_read", _i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                       ctypes.POINTER(ctypes.c_double)]),
 ]

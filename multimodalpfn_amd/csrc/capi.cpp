@@ -556,83 +556,93 @@ void cache_release(mmpfn_cache* cc) {
   delete cc;
 }
 
-int run_layer(mmpfn_ctx* ctx, int l) {
+// ---- attention between features (layer.py:332-339): X [M][T][S][E] <- LN(X + FeatAttn(X)), batch = row s
+int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int S, int T, int M, int prec) {
   const mmpfn_model_desc& d = ctx->d;
-  const LayerW& L = ctx->layers[l];
-  const int S = ctx->S, T = ctx->T, N = ctx->N, Npad = ctx->Npad, prec = ctx->prec, M = ctx->M;
-  const int E = d.emsize, H = d.nhead, Q = S - N;
-  const int64_t R = (int64_t)S * T;  // tokens of one member
-  const int64_t RM = R * M;          // tokens of the batch
-  const int TM = T * M;              // token columns of the batch (attention batches)
+  const int E = d.emsize, H = d.nhead;
+  const int64_t R = (int64_t)S * T;
   const bool bf = prec == PREC_BF16;
   const int eb = bf ? 2 : 4;
   hipStream_t st = ctx->stream;
-  float* Xall = (float*)ctx->ws_X.p;
   void* O = ctx->ws_O.p;
   unsigned char* big = (unsigned char*)ctx->ws_big.p;
-
-  // ---- attention between features (layer.py:332-339): batch = row s, T tokens
   if (bf && L.feat_pack_h.p && T <= 64) {
     // one wave per row (all M members' rows in one launch), the whole sublayer in registers (featrow.hip)
     HIPCHK(launch_feat_rows(Xall, L.feat_pack_h.p, S, T, M, E, H, d.ln_eps, st));
-  } else {
-    for (int m = 0; m < M; ++m) {  // member by member (the scratch holds one member)
-      float* X = Xall + (size_t)m * R * E;
-      if (bf && d.nhead * 32 == E && feat_block_rows(T) > 0) {
-        HIPCHK(launch_feat_block(X, L.feat_qkv_h.p, L.feat_out_h.p, S, T, E, H, d.ln_eps, st));
-        continue;
-      }
-      const int Tpad = (T + 63) / 64 * 64;
-      void* Qf = big;
-      void* Kf = big + (size_t)R * E * eb;
-      void* Vf = (unsigned char*)Kf + (size_t)S * H * Tpad * 32 * eb;
-      GemmArgs a = gargs();
-      // logical rows m = s*T + t: A row t*S + s; scatter batch b = s, position t
-      a.A = X, a.lda = E, a.a_rdiv = T, a.a_rmul = 1, a.a_rmul2 = S;
-      a.W = W(L.feat_qkv, L.feat_qkv_h, prec);
-      a.M = (int)R, a.N = 3 * E, a.K = E;
-      a.q = Qf, a.k = Kf, a.v = Vf, a.S = T, a.Npad = Tpad, a.T = T, a.H = H;
-      HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
-      AttnArgs f;
-      f.q = Qf, f.k = Kf, f.vt = Vf, f.o = O;
-      f.q_bstride = (int64_t)H * T * 32, f.q_hstride = (int64_t)T * 32;
-      f.kv_bstride = (int64_t)H * Tpad * 32, f.kv_hstride = (int64_t)Tpad * 32, f.kpad = Tpad;
-      f.o_bstride = 1, f.o_qstride = S;  // O[t][s]
-      f.s0 = 0, f.nq = T, f.nk = T, f.kvh_fixed = -1, f.H = H;
-      HIPCHK(launch_attn(f, S, prec, 1, st));
-      GemmArgs b = gargs();
-      b.A = O, b.lda = E, b.W = W(L.feat_out, L.feat_out_h, prec);
-      b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
-      HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
-    }
+    return MMPFN_OK;
   }
-  // ---- attention between items (layer.py:341-379); rows of all members: logical row
-  //      (member*T + t)*N + n -> memory row (member*T + t)*S + n, attention batch member*T + t
-  {
-    void* Qi = big;
-    void* Ki = big + (size_t)RM * E * eb;
-    void* Vi = (unsigned char*)Ki + (size_t)TM * H * Npad * 32 * eb;
-    if (ctx->cache_in) {  // every row is a test row: Q only, against the cached train K/V of head 0
-      const mmpfn_cache* cc = ctx->cache_in;
-      const size_t kvl = (size_t)T * cc->Npad * 32 * eb;
-      const unsigned char* Kc = (const unsigned char*)cc->kv.p + (size_t)l * 2 * kvl;
-      const unsigned char* Vc = Kc + kvl;
-      if (bf && E == 192) {
-        HIPCHK(launch_rowgemm_qkv(Xall, S, S, 1, 0, L.item_qtest_h.p, TM * S, E, Qi, Ki, Vi, S, Npad, H, st));
-      } else {
-        GemmArgs c = gargs();
-        c.A = Xall, c.lda = E, c.a_rdiv = S, c.a_rmul = S, c.a_roff = 0;
-        c.W = W(L.item_qtest, L.item_qtest_h, prec);
-        c.M = TM * S, c.N = E, c.K = E;
-        c.q = Qi, c.k = Ki, c.v = Vi, c.S = S, c.Npad = Npad, c.T = TM, c.H = H;
-        HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
-      }
-      const int64_t cstride = (int64_t)cc->Npad * 32;
-      if (bf)
-        HIPCHK(launch_attn_item2(Qi, Kc, Vc, O, S, TM, H, cc->Npad, cc->N, 0, 0, 0, S, 0, st, cstride));
-      else
-        HIPCHK(launch_attn_item(Qi, Kc, Vc, O, S, TM, H, cc->Npad, 0, S, cc->N, 0, prec, st, cstride));
+  for (int m = 0; m < M; ++m) {  // member by member (the scratch holds one member)
+    float* X = Xall + (size_t)m * R * E;
+    if (bf && d.nhead * 32 == E && feat_block_rows(T) > 0) {
+      HIPCHK(launch_feat_block(X, L.feat_qkv_h.p, L.feat_out_h.p, S, T, E, H, d.ln_eps, st));
+      continue;
+    }
+    const int Tpad = (T + 63) / 64 * 64;
+    void* Qf = big;
+    void* Kf = big + (size_t)R * E * eb;
+    void* Vf = (unsigned char*)Kf + (size_t)S * H * Tpad * 32 * eb;
+    GemmArgs a = gargs();
+    // logical rows m = s*T + t: A row t*S + s; scatter batch b = s, position t
+    a.A = X, a.lda = E, a.a_rdiv = T, a.a_rmul = 1, a.a_rmul2 = S;
+    a.W = W(L.feat_qkv, L.feat_qkv_h, prec);
+    a.M = (int)R, a.N = 3 * E, a.K = E;
+    a.q = Qf, a.k = Kf, a.v = Vf, a.S = T, a.Npad = Tpad, a.T = T, a.H = H;
+    HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+    AttnArgs f;
+    f.q = Qf, f.k = Kf, f.vt = Vf, f.o = O;
+    f.q_bstride = (int64_t)H * T * 32, f.q_hstride = (int64_t)T * 32;
+    f.kv_bstride = (int64_t)H * Tpad * 32, f.kv_hstride = (int64_t)Tpad * 32, f.kpad = Tpad;
+    f.o_bstride = 1, f.o_qstride = S;  // O[t][s]
+    f.s0 = 0, f.nq = T, f.nk = T, f.kvh_fixed = -1, f.H = H;
+    HIPCHK(launch_attn(f, S, prec, 1, st));
+    GemmArgs b = gargs();
+    b.A = O, b.lda = E, b.W = W(L.feat_out, L.feat_out_h, prec);
+    b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
+    HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
+  }
+  return MMPFN_OK;
+}
+
+// ---- attention between items (layer.py:341-379) of layer l; rows of all members: logical row
+//      (member*T + t)*N + n -> memory row (member*T + t)*S + n, attention batch member*T + t.
+//      fuse_out: the out-projection + residual + LN is left to the MLP kernel's prologue (the
+//      attention output stays in ws_O); otherwise X <- LN(X + O Wout^T) here.
+int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int Npad, int M, int prec,
+                  bool fuse_out) {
+  const mmpfn_model_desc& d = ctx->d;
+  const LayerW& L = ctx->layers[l];
+  const int E = d.emsize, H = d.nhead, Q = S - N;
+  const int64_t RM = (int64_t)S * T * M;  // tokens of the batch
+  const int TM = T * M;                   // token columns of the batch (attention batches)
+  const bool bf = prec == PREC_BF16;
+  const int eb = bf ? 2 : 4;
+  hipStream_t st = ctx->stream;
+  void* O = ctx->ws_O.p;
+  unsigned char* big = (unsigned char*)ctx->ws_big.p;
+  void* Qi = big;
+  void* Ki = big + (size_t)RM * E * eb;
+  void* Vi = (unsigned char*)Ki + (size_t)TM * H * Npad * 32 * eb;
+  if (ctx->cache_in) {  // every row is a test row: Q only, against the cached train K/V of head 0
+    const mmpfn_cache* cc = ctx->cache_in;
+    const size_t kvl = (size_t)T * cc->Npad * 32 * eb;
+    const unsigned char* Kc = (const unsigned char*)cc->kv.p + (size_t)l * 2 * kvl;
+    const unsigned char* Vc = Kc + kvl;
+    if (bf && E == 192) {
+      HIPCHK(launch_rowgemm_qkv(Xall, S, S, 1, 0, L.item_qtest_h.p, TM * S, E, Qi, Ki, Vi, S, Npad, H, st));
     } else {
+      GemmArgs c = gargs();
+      c.A = Xall, c.lda = E, c.a_rdiv = S, c.a_rmul = S, c.a_roff = 0;
+      c.W = W(L.item_qtest, L.item_qtest_h, prec);
+      c.M = TM * S, c.N = E, c.K = E;
+      c.q = Qi, c.k = Ki, c.v = Vi, c.S = S, c.Npad = Npad, c.T = TM, c.H = H;
+      HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+    }
+    const int64_t cstride = (int64_t)cc->Npad * 32;
+    if (bf)
+      HIPCHK(launch_attn_item2(Qi, Kc, Vc, O, S, TM, H, cc->Npad, cc->N, 0, 0, 0, S, 0, st, cstride));
+    else
+      HIPCHK(launch_attn_item(Qi, Kc, Vc, O, S, TM, H, cc->Npad, 0, S, cc->N, 0, prec, st, cstride));
+  } else {
     if (bf && E == 192) {  // row-resident projections straight into the attention layouts
       HIPCHK(launch_rowgemm_qkv(Xall, N, S, 1, 0, L.item_qkv_h.p, TM * N, 3 * E, Qi, Ki, Vi, S, Npad, H, st));
       if (Q > 0)
@@ -680,24 +690,50 @@ int run_layer(mmpfn_ctx* ctx, int l) {
       HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, 0, N, N, -1, prec, st));
       if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, N, Q, N, 0, prec, st));
     }
-    }
-    if (bf && E == 192 && d.nhid % 32 == 0) {
-      // the out-projection + residual + LN runs as the prologue of the MLP kernel below
-    } else if (bf && E == 192) {
-      HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, RM, Xall, d.ln_eps, st));
-    } else {
-      GemmArgs b = gargs();
-      b.A = O, b.lda = E, b.W = W(L.item_out, L.item_out_h, prec);
-      b.M = (int)RM, b.N = E, b.K = E, b.X = Xall, b.ln_eps = d.ln_eps;
-      HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
-    }
   }
-  // ---- MLP (mlp.py:93-104), fused up/GELU/down/residual/LN, all members' tokens
-  if (bf && E == 192 && d.nhid % 32 == 0)  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders; fused out-proj
-    HIPCHK(launch_mlp_rows(Xall, L.mlp1_h.p, L.mlp2_h.p, RM, E, d.nhid, d.ln_eps, st, ctx->ws_O.p,
-                           L.item_out_h.p));
+  if (fuse_out) return MMPFN_OK;
+  if (bf && E == 192) {
+    HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, RM, Xall, d.ln_eps, st));
+  } else {
+    GemmArgs b = gargs();
+    b.A = O, b.lda = E, b.W = W(L.item_out, L.item_out_h, prec);
+    b.M = (int)RM, b.N = E, b.K = E, b.X = Xall, b.ln_eps = d.ln_eps;
+    HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
+  }
+  return MMPFN_OK;
+}
+
+// the bf16 MLP kernel runs the item-attention out-projection as its prologue
+bool mlp_fuses_out(const mmpfn_model_desc& d, int prec) { return prec == PREC_BF16 && d.emsize == 192 && d.nhid % 32 == 0; }
+
+// ---- MLP (mlp.py:93-104) + residual + LN over RM tokens; O non-null: the fused out-projection first
+int mlp_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int64_t RM, int prec, const void* O) {
+  const mmpfn_model_desc& d = ctx->d;
+  if (mlp_fuses_out(d, prec))  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders
+    HIPCHK(launch_mlp_rows(Xall, L.mlp1_h.p, L.mlp2_h.p, RM, d.emsize, d.nhid, d.ln_eps, ctx->stream, O,
+                           O ? L.item_out_h.p : nullptr));
   else
-    HIPCHK(launch_mlp_fused(Xall, L.mlp1.p, L.mlp2.p, RM, E, d.nhid, d.ln_eps, PREC_F32, st));
+    HIPCHK(launch_mlp_fused(Xall, L.mlp1.p, L.mlp2.p, RM, d.emsize, d.nhid, d.ln_eps, PREC_F32, ctx->stream));
+  return MMPFN_OK;
+}
+
+int run_layer(mmpfn_ctx* ctx, int l) {
+  const LayerW& L = ctx->layers[l];
+  const int S = ctx->S, T = ctx->T, N = ctx->N, Npad = ctx->Npad, prec = ctx->prec, M = ctx->M;
+  float* Xall = (float*)ctx->ws_X.p;
+  const bool fuse = mlp_fuses_out(ctx->d, prec);
+  RC(feat_sublayer(ctx, L, Xall, S, T, M, prec));
+  RC(item_sublayer(ctx, l, Xall, S, T, N, Npad, M, prec, fuse));
+  return mlp_sublayer(ctx, L, Xall, (int64_t)S * T * M, prec, fuse ? ctx->ws_O.p : nullptr);
+}
+
+// workspace of the selected lane for a per-sublayer tap on a caller-provided state of S x T tokens
+int tap_workspace(mmpfn_ctx* ctx, int S, int T, int Npad) {
+  const int E = ctx->d.emsize;
+  const size_t R = (size_t)S * T;
+  const size_t Tpad = (T + 63) / 64 * 64;
+  RC(ensure(ctx, ctx->ws_O, R * E * 4));
+  RC(ensure(ctx, ctx->ws_big, std::max(R * E + 2 * S * Tpad * E, R * E + (size_t)2 * T * Npad * E) * 4));
   return MMPFN_OK;
 }
 
@@ -714,78 +750,94 @@ int decode(mmpfn_ctx* ctx, float* logits, int M = 1) {
   return MMPFN_OK;
 }
 
-int mixer(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int prec) {
+// MGM head bank (transformer.py:33-57): image [S][n_mod][D] -> tokens [S][mgm*n_mod][E] (head-major)
+int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* mtok, int prec) {
   const mmpfn_model_desc& d = ctx->d;
   const int E = d.emsize, D = d.nhid;
   const bool bf = prec == PREC_BF16;
   const int eb = bf ? 2 : 4;
   hipStream_t st = ctx->stream;
   const int64_t rows = (int64_t)S * n_mod;
-  if (d.mixer_type == MMPFN_MIXER_MGM || d.mixer_type == MMPFN_MIXER_MGM_CAP) {
-    const int mg = d.mgm_heads, M = mg * n_mod;
-    RC(ensure(ctx, ctx->mx[0], (size_t)rows * D * eb));               // normalised image
-    RC(ensure(ctx, ctx->mx[1], (size_t)rows * mg * (D / 2) * eb));    // GLU output
-    const bool final_mgm = d.mixer_type == MMPFN_MIXER_MGM;
-    float* mtok = final_mgm ? tokens : nullptr;
-    if (!final_mgm) {
-      RC(ensure(ctx, ctx->mx[2], (size_t)S * M * E * 4));
-      mtok = (float*)ctx->mx[2].p;
-    }
-    HIPCHK(launch_layernorm_rows(image, rows, D, 1e-5f, ctx->mx[0].p, !bf, nullptr, nullptr, st));
-    GemmArgs a = gargs();
-    a.A = ctx->mx[0].p, a.lda = D, a.W = W(ctx->mgm_w1, ctx->mgm_w1_h, prec), a.bias = (const float*)ctx->mgm_b1.p;
-    a.M = (int)rows, a.N = mg * D, a.K = D, a.C = ctx->mx[1].p, a.ldc = (int64_t)mg * (D / 2);
-    if (bf && (mg * D) % 256 == 0 && D % 64 == 0)
-      HIPCHK(launch_gemm_glu_big(ctx->mx[0].p, a.W, a.bias, ctx->mx[1].p, (int)rows, mg * D, D, st));
-    else
-      HIPCHK(launch_gemm(a, prec, EPI_GLU, !bf, !bf, 1, st));
-    GemmArgs b = gargs();
-    b.A = ctx->mx[1].p, b.lda = (int64_t)mg * (D / 2), b.a_zstride = D / 2;
-    b.W = W(ctx->mgm_w2, ctx->mgm_w2_h, prec), b.w_zstride = (int64_t)E * (D / 2);
-    b.bias = (const float*)ctx->mgm_b2.p, b.b_zstride = E;
-    b.M = (int)rows, b.N = E, b.K = D / 2;
-    b.C = mtok, b.ldc = E, b.rdiv2 = n_mod, b.rmul2 = M, b.zmul = n_mod;
-    HIPCHK(launch_gemm(b, prec, EPI_REMAP, !bf, true, mg, st));
-    if (final_mgm) return MMPFN_OK;
-    // ---- CAP (transformer.py:77-88)
-    const int cap = d.cap_heads;
-    const int64_t srows = (int64_t)S * M;
-    RC(ensure(ctx, ctx->mx[3], (size_t)srows * E * eb));        // k_norm(src) (affine folded)
-    RC(ensure(ctx, ctx->mx[4], (size_t)srows * 2 * E * eb));    // K|V
-    RC(ensure(ctx, ctx->mx[5], (size_t)S * cap * E * 4));       // attention out (heads concat)
-    RC(ensure(ctx, ctx->mx[6], (size_t)S * cap * E * 4));       // out_proj
-    RC(ensure(ctx, ctx->mx[7], (size_t)S * cap * 2 * E * 4));   // ffn hidden (+ ffn out after)
-    if (bf && E == 192) {  // k_norm + K|V projection in one row pass (normalised rows stay in registers)
-      HIPCHK(launch_rowgemm_ln_store(mtok, ctx->cap_kv_h.p, (const float*)ctx->cap_kv_b.p, ctx->mx[4].p, srows, 2 * E,
-                                     1e-5f, true, st));
-    } else {
-      HIPCHK(launch_layernorm_rows(mtok, srows, E, 1e-5f, ctx->mx[3].p, !bf, nullptr, nullptr, st));
-      GemmArgs c = gargs();
-      c.A = ctx->mx[3].p, c.lda = E, c.W = W(ctx->cap_kv, ctx->cap_kv_h, prec), c.bias = (const float*)ctx->cap_kv_b.p;
-      c.M = (int)srows, c.N = 2 * E, c.K = E, c.C = ctx->mx[4].p, c.ldc = 2 * E;
-      HIPCHK(launch_gemm(c, prec, EPI_STORE, !bf, !bf, 1, st));
-    }
-    HIPCHK(launch_cap_attention((const float*)ctx->cap_qp.p, ctx->mx[4].p, !bf, (float*)ctx->mx[5].p, S, M, cap, E,
-                                st));
-    const int64_t crow = (int64_t)S * cap;
-    // projections run in fp32 A (tiny); bf16 weights in perf mode
-    GemmArgs o = gargs();
-    o.A = ctx->mx[5].p, o.lda = E, o.W = W(ctx->cap_o, ctx->cap_o_h, prec), o.bias = (const float*)ctx->cap_o_b.p;
-    o.M = (int)crow, o.N = E, o.K = E, o.C = ctx->mx[6].p, o.ldc = E;
-    HIPCHK(launch_gemm(o, prec, EPI_STORE, true, true, 1, st));
-    GemmArgs f0 = gargs();
-    f0.A = ctx->mx[6].p, f0.lda = E, f0.W = W(ctx->cap_f0, ctx->cap_f0_h, prec);
-    f0.bias = (const float*)ctx->cap_f0_b.p, f0.act = ACT_GELU;
-    f0.M = (int)crow, f0.N = 2 * E, f0.K = E, f0.C = ctx->mx[7].p, f0.ldc = 2 * E;
-    HIPCHK(launch_gemm(f0, prec, EPI_STORE, true, true, 1, st));
-    GemmArgs f3 = gargs();
-    f3.A = ctx->mx[7].p, f3.lda = 2 * E, f3.W = W(ctx->cap_f3, ctx->cap_f3_h, prec);
-    f3.bias = (const float*)ctx->cap_f3_b.p;
-    f3.M = (int)crow, f3.N = E, f3.K = 2 * E, f3.C = ctx->mx[5].p, f3.ldc = E;  // reuse mx5 for ffn out
-    HIPCHK(launch_gemm(f3, prec, EPI_STORE, true, true, 1, st));
-    HIPCHK(launch_ln_add((const float*)ctx->mx[6].p, (const float*)ctx->mx[5].p, (const float*)ctx->cap_ng.p,
-                         (const float*)ctx->cap_nb.p, tokens, crow, E, 1e-5f, st));
-    return MMPFN_OK;
+  const int mg = d.mgm_heads, M = mg * n_mod;
+  RC(ensure(ctx, ctx->mx[0], (size_t)rows * D * eb));             // normalised image
+  RC(ensure(ctx, ctx->mx[1], (size_t)rows * mg * (D / 2) * eb));  // GLU output
+  HIPCHK(launch_layernorm_rows(image, rows, D, 1e-5f, ctx->mx[0].p, !bf, nullptr, nullptr, st));
+  GemmArgs a = gargs();
+  a.A = ctx->mx[0].p, a.lda = D, a.W = W(ctx->mgm_w1, ctx->mgm_w1_h, prec), a.bias = (const float*)ctx->mgm_b1.p;
+  a.M = (int)rows, a.N = mg * D, a.K = D, a.C = ctx->mx[1].p, a.ldc = (int64_t)mg * (D / 2);
+  if (bf && (mg * D) % 256 == 0 && D % 64 == 0)
+    HIPCHK(launch_gemm_glu_big(ctx->mx[0].p, a.W, a.bias, ctx->mx[1].p, (int)rows, mg * D, D, st));
+  else
+    HIPCHK(launch_gemm(a, prec, EPI_GLU, !bf, !bf, 1, st));
+  GemmArgs b = gargs();
+  b.A = ctx->mx[1].p, b.lda = (int64_t)mg * (D / 2), b.a_zstride = D / 2;
+  b.W = W(ctx->mgm_w2, ctx->mgm_w2_h, prec), b.w_zstride = (int64_t)E * (D / 2);
+  b.bias = (const float*)ctx->mgm_b2.p, b.b_zstride = E;
+  b.M = (int)rows, b.N = E, b.K = D / 2;
+  b.C = mtok, b.ldc = E, b.rdiv2 = n_mod, b.rmul2 = M, b.zmul = n_mod;
+  HIPCHK(launch_gemm(b, prec, EPI_REMAP, !bf, true, mg, st));
+  return MMPFN_OK;
+}
+
+// CrossAttentionPooler (transformer.py:60-88): MGM tokens [S][M][E] -> tokens [S][cap][E]
+int mixer_cap(mmpfn_ctx* ctx, const float* mtok, int S, int M, float* tokens, int prec) {
+  const mmpfn_model_desc& d = ctx->d;
+  const int E = d.emsize;
+  const bool bf = prec == PREC_BF16;
+  const int eb = bf ? 2 : 4;
+  hipStream_t st = ctx->stream;
+  const int cap = d.cap_heads;
+  const int64_t srows = (int64_t)S * M;
+  RC(ensure(ctx, ctx->mx[3], (size_t)srows * E * eb));        // k_norm(src) (affine folded)
+  RC(ensure(ctx, ctx->mx[4], (size_t)srows * 2 * E * eb));    // K|V
+  RC(ensure(ctx, ctx->mx[5], (size_t)S * cap * E * 4));       // attention out (heads concat)
+  RC(ensure(ctx, ctx->mx[6], (size_t)S * cap * E * 4));       // out_proj
+  RC(ensure(ctx, ctx->mx[7], (size_t)S * cap * 2 * E * 4));   // ffn hidden (+ ffn out after)
+  if (bf && E == 192) {  // k_norm + K|V projection in one row pass (normalised rows stay in registers)
+    HIPCHK(launch_rowgemm_ln_store(mtok, ctx->cap_kv_h.p, (const float*)ctx->cap_kv_b.p, ctx->mx[4].p, srows, 2 * E,
+                                   1e-5f, true, st));
+  } else {
+    HIPCHK(launch_layernorm_rows(mtok, srows, E, 1e-5f, ctx->mx[3].p, !bf, nullptr, nullptr, st));
+    GemmArgs c = gargs();
+    c.A = ctx->mx[3].p, c.lda = E, c.W = W(ctx->cap_kv, ctx->cap_kv_h, prec), c.bias = (const float*)ctx->cap_kv_b.p;
+    c.M = (int)srows, c.N = 2 * E, c.K = E, c.C = ctx->mx[4].p, c.ldc = 2 * E;
+    HIPCHK(launch_gemm(c, prec, EPI_STORE, !bf, !bf, 1, st));
+  }
+  HIPCHK(launch_cap_attention((const float*)ctx->cap_qp.p, ctx->mx[4].p, !bf, (float*)ctx->mx[5].p, S, M, cap, E,
+                              st));
+  const int64_t crow = (int64_t)S * cap;
+  // projections run in fp32 A (tiny); bf16 weights in perf mode
+  GemmArgs o = gargs();
+  o.A = ctx->mx[5].p, o.lda = E, o.W = W(ctx->cap_o, ctx->cap_o_h, prec), o.bias = (const float*)ctx->cap_o_b.p;
+  o.M = (int)crow, o.N = E, o.K = E, o.C = ctx->mx[6].p, o.ldc = E;
+  HIPCHK(launch_gemm(o, prec, EPI_STORE, true, true, 1, st));
+  GemmArgs f0 = gargs();
+  f0.A = ctx->mx[6].p, f0.lda = E, f0.W = W(ctx->cap_f0, ctx->cap_f0_h, prec);
+  f0.bias = (const float*)ctx->cap_f0_b.p, f0.act = ACT_GELU;
+  f0.M = (int)crow, f0.N = 2 * E, f0.K = E, f0.C = ctx->mx[7].p, f0.ldc = 2 * E;
+  HIPCHK(launch_gemm(f0, prec, EPI_STORE, true, true, 1, st));
+  GemmArgs f3 = gargs();
+  f3.A = ctx->mx[7].p, f3.lda = 2 * E, f3.W = W(ctx->cap_f3, ctx->cap_f3_h, prec);
+  f3.bias = (const float*)ctx->cap_f3_b.p;
+  f3.M = (int)crow, f3.N = E, f3.K = 2 * E, f3.C = ctx->mx[5].p, f3.ldc = E;  // reuse mx5 for ffn out
+  HIPCHK(launch_gemm(f3, prec, EPI_STORE, true, true, 1, st));
+  HIPCHK(launch_ln_add((const float*)ctx->mx[6].p, (const float*)ctx->mx[5].p, (const float*)ctx->cap_ng.p,
+                       (const float*)ctx->cap_nb.p, tokens, crow, E, 1e-5f, st));
+  return MMPFN_OK;
+}
+
+int mixer(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int prec) {
+  const mmpfn_model_desc& d = ctx->d;
+  const int E = d.emsize, D = d.nhid;
+  const bool bf = prec == PREC_BF16;
+  const int eb = bf ? 2 : 4;
+  hipStream_t st = ctx->stream;
+  if (d.mixer_type == MMPFN_MIXER_MGM) return mixer_mgm(ctx, image, S, n_mod, tokens, prec);
+  if (d.mixer_type == MMPFN_MIXER_MGM_CAP) {
+    const int M = d.mgm_heads * n_mod;
+    RC(ensure(ctx, ctx->mx[2], (size_t)S * M * E * 4));
+    RC(mixer_mgm(ctx, image, S, n_mod, (float*)ctx->mx[2].p, prec));
+    return mixer_cap(ctx, (const float*)ctx->mx[2].p, S, M, tokens, prec);
   }
   if (d.mixer_type == MMPFN_MIXER_MOE) {
     const int ne = d.mgm_heads;
@@ -1148,6 +1200,56 @@ int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, con
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(launch_attn_item2(q, k, vt, out, S, T, H, Npad, N, 0, N, N, S - N, 0, ctx->stream));
   return MMPFN_OK;
+}
+
+// ---- per-sublayer taps ------------------------------------------------------------
+static int tap_check(mmpfn_ctx* ctx, int layer, const void* X, int precision) {
+  if (!ctx || !X) return MMPFN_ERR_INVALID;
+  if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
+  if (layer < 0 || layer >= ctx->d.nlayers) return fail(ctx, MMPFN_ERR_INVALID, "bad layer index");
+  if (precision != PREC_F32 && precision != PREC_BF16) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  HIPCHK(hipSetDevice(ctx->device));
+  return MMPFN_OK;
+}
+
+int mmpfn_feature_attention(mmpfn_ctx* ctx, int layer, float* X, int S, int T, int precision) {
+  RC(tap_check(ctx, layer, X, precision));
+  if (S <= 0 || T <= 0) return fail(ctx, MMPFN_ERR_INVALID, "bad state geometry");
+  RC(tap_workspace(ctx, S, T, 64));
+  return feat_sublayer(ctx, ctx->layers[layer], X, S, T, 1, precision);
+}
+
+int mmpfn_item_attention_block(mmpfn_ctx* ctx, int layer, float* X, int S, int T, int N, int precision) {
+  RC(tap_check(ctx, layer, X, precision));
+  if (S <= 0 || T <= 0 || N <= 0 || N > S) return fail(ctx, MMPFN_ERR_INVALID, "bad state geometry");
+  const int Npad = (N + 63) / 64 * 64;
+  RC(tap_workspace(ctx, S, T, Npad));
+  return item_sublayer(ctx, layer, X, S, T, N, Npad, 1, precision, false);
+}
+
+int mmpfn_mlp_ln(mmpfn_ctx* ctx, int layer, float* X, int64_t rows, int precision) {
+  RC(tap_check(ctx, layer, X, precision));
+  if (rows <= 0) return fail(ctx, MMPFN_ERR_INVALID, "bad row count");
+  return mlp_sublayer(ctx, ctx->layers[layer], X, rows, precision, nullptr);
+}
+
+int mmpfn_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int precision) {
+  if (!ctx || !image || !tokens || S <= 0 || n_mod <= 0) return MMPFN_ERR_INVALID;
+  if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
+  if (ctx->d.mixer_type != MMPFN_MIXER_MGM && ctx->d.mixer_type != MMPFN_MIXER_MGM_CAP)
+    return fail(ctx, MMPFN_ERR_INVALID, "model has no MGM head bank");
+  if (precision != PREC_F32 && precision != PREC_BF16) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  HIPCHK(hipSetDevice(ctx->device));
+  return mixer_mgm(ctx, image, S, n_mod, tokens, precision);
+}
+
+int mmpfn_cap(mmpfn_ctx* ctx, const float* mgm_tokens, int S, int M, float* tokens, int precision) {
+  if (!ctx || !mgm_tokens || !tokens || S <= 0 || M <= 0) return MMPFN_ERR_INVALID;
+  if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
+  if (ctx->d.mixer_type != MMPFN_MIXER_MGM_CAP) return fail(ctx, MMPFN_ERR_INVALID, "model has no CAP");
+  if (precision != PREC_F32 && precision != PREC_BF16) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  HIPCHK(hipSetDevice(ctx->device));
+  return mixer_cap(ctx, mgm_tokens, S, M, tokens, precision);
 }
 
 }  // extern "C"

@@ -424,6 +424,54 @@ class HipEngine:
         torch.cuda.current_stream(self.device).synchronize()
         return out
 
+    # ------------------------------------------------------------------ per-sublayer taps
+    def _state_tap(self, X: torch.Tensor, fn, argf) -> torch.Tensor:
+        """Run a C-ABI sublayer tap on a reference-order state ``[S, T, E]`` (copied to the
+        engine's token-major ``[T, S, E]``, updated in place, copied back)."""
+        Xt = self._dev(X).transpose(0, 1).contiguous()
+        T, S, _ = Xt.shape
+        self._bind_stream()
+        self._check(fn(self.ctx, *argf(Xt, S, T)), fn.__name__)
+        return Xt.transpose(0, 1).contiguous()
+
+    def feature_attention(self, layer: int, X: torch.Tensor, precision: int) -> torch.Tensor:
+        """``LN(X + FeatAttn_layer(X))`` (layer.py:332-339) through ``mmpfn_feature_attention``."""
+        return self._state_tap(X, self.lib.mmpfn_feature_attention,
+                               lambda Xt, S, T: (layer, _ptr(Xt), S, T, precision))
+
+    def item_attention_block(self, layer: int, X: torch.Tensor, n_train: int, precision: int) -> torch.Tensor:
+        """``LN(X + ItemAttn_layer(X))`` (layer.py:341-379) through ``mmpfn_item_attention_block``."""
+        return self._state_tap(X, self.lib.mmpfn_item_attention_block,
+                               lambda Xt, S, T: (layer, _ptr(Xt), S, T, n_train, precision))
+
+    def mlp_ln(self, layer: int, X: torch.Tensor, precision: int) -> torch.Tensor:
+        """``LN(X + MLP_layer(X))`` (mlp.py:93-138) through ``mmpfn_mlp_ln`` (row-wise: any order)."""
+        Xd = self._dev(X).contiguous().clone()
+        self._bind_stream()
+        self._check(self.lib.mmpfn_mlp_ln(self.ctx, layer, _ptr(Xd), Xd.numel() // self.cfg.emsize, precision),
+                    "mmpfn_mlp_ln")
+        return Xd
+
+    def mgm(self, image, precision: int) -> torch.Tensor:
+        """MultiheadGatedMLP tokens ``[S, mgm * n_mod, E]`` (transformer.py:33-57)."""
+        img = self._dev(image)
+        if img.dim() == 2:
+            img = img.unsqueeze(1)
+        S, n_mod, _ = img.shape
+        out = torch.empty((S, self.cfg.mgm_heads * n_mod, self.cfg.emsize), device=self.device)
+        self._bind_stream()
+        self._check(self.lib.mmpfn_mgm(self.ctx, _ptr(img), S, n_mod, _ptr(out), precision), "mmpfn_mgm")
+        return out
+
+    def cap(self, mgm_tokens, precision: int) -> torch.Tensor:
+        """CrossAttentionPooler tokens ``[S, cap, E]`` (transformer.py:60-88)."""
+        tok = self._dev(mgm_tokens)
+        S, M, _ = tok.shape
+        out = torch.empty((S, self.cfg.cap_heads, self.cfg.emsize), device=self.device)
+        self._bind_stream()
+        self._check(self.lib.mmpfn_cap(self.ctx, _ptr(tok), S, M, _ptr(out), precision), "mmpfn_cap")
+        return out
+
     def decode(self, n_query: int) -> torch.Tensor:
         out = torch.empty((n_query, self.cfg.n_out), device=self.device, dtype=torch.float32)
         self._bind_stream()

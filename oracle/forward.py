@@ -225,7 +225,16 @@ def oracle_mixer(spec: OracleSpec, w: dict, image: torch.Tensor) -> torch.Tensor
             outs.append((probs[:, i : i + 1] * h).unsqueeze(-2))
         return torch.cat(outs, dim=-2)
 
-    # MGM
+    tok = oracle_mgm(spec, w, image)
+    if spec.mixer_type == "MGM":
+        return tok
+    assert spec.mixer_type == "MGM+CAP"
+    return oracle_cap(spec, w, tok)
+
+
+def oracle_mgm(spec: OracleSpec, w: dict, image: torch.Tensor) -> torch.Tensor:
+    """MultiheadGatedMLP (T/transformer.py:33-57): ``[S, n_mod, 768]`` -> ``[S, mgm*n_mod, E]``."""
+    dt = image.dtype
     outs = []
     for hh in range(spec.mgm_heads):
         p = f"mgm.projs.{hh}"
@@ -234,11 +243,13 @@ def oracle_mixer(spec: OracleSpec, w: dict, image: torch.Tensor) -> torch.Tensor
         a, b = h.chunk(2, dim=-1)
         h = a * torch.sigmoid(b)  # nn.GLU
         outs.append(_linear(h, w, p + ".4"))
-    tok = torch.cat(outs, dim=-2)  # [S, mgm*n_mod, E]
-    if spec.mixer_type == "MGM":
-        return tok
-    assert spec.mixer_type == "MGM+CAP"
+    return torch.cat(outs, dim=-2)  # [S, mgm*n_mod, E]
 
+
+def oracle_cap(spec: OracleSpec, w: dict, tok: torch.Tensor) -> torch.Tensor:
+    """CrossAttentionPooler (T/transformer.py:60-88): MGM tokens ``[S, M, E]`` -> ``[S, cap, E]``."""
+    dt = tok.dtype
+    S = tok.shape[0]
     E = spec.emsize
     nh = spec.cap_heads
     hd = E // nh
@@ -294,27 +305,24 @@ def _ln(x, eps):
     return F.layer_norm(x, (x.shape[-1],), None, None, eps)
 
 
-def layer_forward(spec: OracleSpec, w: dict, l: int, X: torch.Tensor, n_train: int, use_sdpa=False):
-    """One ``PerFeatureEncoderLayer`` (post-norm; T/layer.py:272-457).
-
-    ``X``: ``[S, T, E]``.  feature-attn -> LN -> item-attn -> LN -> MLP -> LN.
-    """
-    S, T, E = X.shape
-    H = spec.nhead
-    d = E // H
+def feat_sublayer(spec: OracleSpec, w: dict, l: int, X: torch.Tensor, use_sdpa=False):
+    """Attention between features + residual + LN (T/layer.py:332-339,437-455); ``X`` ``[S, T, E]``."""
     dt = X.dtype
     p = f"transformer_encoder.layers.{l}"
-
-    # --- attention between features (self, fused w_qkv; T/multi_head_attention.py:423-430)
-    wqkv = w[p + ".self_attn_between_features._w_qkv"].to(dt)  # [3, H, d, E]
+    wqkv = w[p + ".self_attn_between_features._w_qkv"].to(dt)  # [3, H, d, E] (T/multi_head_attention.py:423-430)
     wout = w[p + ".self_attn_between_features._w_out"].to(dt)  # [H, d, E]
     qkv = torch.einsum("ste,jhde->sjhtd", X, wqkv)  # [S, 3, H, T, d]
     o = _attn(qkv[:, 0], qkv[:, 1], qkv[:, 2], use_sdpa)  # [S, H, T, d]
     o = torch.einsum("shtd,hde->ste", o, wout)
-    X = _ln(X + o, spec.ln_eps)
+    return _ln(X + o, spec.ln_eps)
 
-    # --- attention between items (T/layer.py:341-379), per token column
-    pi = p + ".self_attn_between_items"
+
+def item_sublayer(spec: OracleSpec, w: dict, l: int, X: torch.Tensor, n_train: int, use_sdpa=False):
+    """Attention between items + residual + LN (T/layer.py:341-379,437-455), per token column:
+    train rows on all KV heads, test rows on head 0's K/V broadcast (reuse_first_head_kv)."""
+    S = X.shape[0]
+    dt = X.dtype
+    pi = f"transformer_encoder.layers.{l}.self_attn_between_items"
     if spec.two_sets_of_queries:
         wq_all = w[pi + "._w_q"].to(dt)  # [2, H, d, E]
         wq_tr, wq_te = wq_all[0], wq_all[1]
@@ -339,12 +347,25 @@ def layer_forward(spec: OracleSpec, w: dict, l: int, X: torch.Tensor, n_train: i
         outs.append(_attn(q, k0, v0, use_sdpa))
     o = torch.cat(outs, dim=2)  # [T, H, S, d]
     o = torch.einsum("thsd,hde->ste", o, wout)
-    X = _ln(X + o, spec.ln_eps)
+    return _ln(X + o, spec.ln_eps)
 
-    # --- MLP (T/mlp.py:93-104): Linear(no bias) -> GELU(erf) -> Linear(no bias)
+
+def mlp_sublayer(spec: OracleSpec, w: dict, l: int, X: torch.Tensor):
+    """MLP (T/mlp.py:93-104): Linear(no bias) -> GELU(erf) -> Linear(no bias), residual, LN."""
+    dt = X.dtype
+    p = f"transformer_encoder.layers.{l}"
     h = F.gelu(X @ w[p + ".mlp.linear1.weight"].to(dt).T)
-    X = _ln(X + h @ w[p + ".mlp.linear2.weight"].to(dt).T, spec.ln_eps)
-    return X
+    return _ln(X + h @ w[p + ".mlp.linear2.weight"].to(dt).T, spec.ln_eps)
+
+
+def layer_forward(spec: OracleSpec, w: dict, l: int, X: torch.Tensor, n_train: int, use_sdpa=False):
+    """One ``PerFeatureEncoderLayer`` (post-norm; T/layer.py:272-457).
+
+    ``X``: ``[S, T, E]``.  feature-attn -> LN -> item-attn -> LN -> MLP -> LN.
+    """
+    X = feat_sublayer(spec, w, l, X, use_sdpa)
+    X = item_sublayer(spec, w, l, X, n_train, use_sdpa)
+    return mlp_sublayer(spec, w, l, X)
 
 
 def embed_inputs(spec, w, x, image, y_train, dtype=torch.float32, mixer_tokens=None):

@@ -17,7 +17,7 @@ from oracle.forward import layer_forward, oracle_forward
 pytestmark = pytest.mark.gpu
 
 F32_TOL = 1e-4
-LARGE_BF16_TOL = {"B": 5e-2, "E": 5e-2}
+LARGE_BF16_TOL = {"B": 2.5e-2, "E": 3.5e-2}  # measured 1.28e-2 and 1.80e-2 (profiles/r02)
 BF16_TOL = 2e-2  # measured 3.1e-3 .. 9.5e-3 over the goldens (profiles/r02/pytest_gpu_r02a.log)
 
 

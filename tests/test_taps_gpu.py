@@ -1,0 +1,100 @@
+"""GPU: every per-sublayer C-ABI tap (include/mmpfn_hip.h) against the oracle's matching function.
+
+Inputs are the oracle's own intermediate states of a golden case (so each tap is checked in
+isolation), plus config-C-sized states for the kernels' production shapes.  Tolerances:
+fp32 parity mode <= 2e-5 relative to max(1, max|ref|) per sublayer (the oracle runs fp64);
+bf16 mode <= 2e-2 (bf16 operands, fp32 accumulation / LayerNorm).
+"""
+
+import pytest
+import torch
+
+from helpers import load_case, oracle_spec, rel_err, torch_sd
+from oracle.forward import embed_inputs, feat_sublayer, item_sublayer, mlp_sublayer, oracle_cap, oracle_mgm
+
+pytestmark = pytest.mark.gpu
+
+TOL = {0: 2e-5, 1: 2e-2}
+
+
+def _engine(cfg, sd):
+    from multimodalpfn_amd.model.transformer import PerFeatureTransformer
+
+    model = PerFeatureTransformer(cfg)
+    model.load_state_dict(torch_sd(sd))
+    norm = next(e for e in model.encoder if "InputNormalizationEncoderStep" in str(e.__class__))
+    norm.remove_outliers, norm.remove_outliers_sigma = True, cfg.remove_outliers_sigma or 12.0
+    return model.to("cuda").engine()
+
+
+def _golden_states(case):
+    z, meta, cfg, sd = load_case(case)
+    spec, w = oracle_spec(cfg), torch_sd(sd)
+    x = torch.from_numpy(z["x"]) if "x" in z else None
+    im = torch.from_numpy(z["image"]) if "image" in z else None
+    y = torch.from_numpy(z["y_train"])
+    X0 = embed_inputs(spec, w, x, im, y, dtype=torch.float64)
+    return cfg, sd, spec, {k: v.double() for k, v in w.items()}, X0, len(y), im
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("case", ["mgmcap_edge", "pad_ufes_12l", "two_queries"])
+def test_layer_sublayer_taps_match_oracle(case, prec):
+    cfg, sd, spec, w, X0, N, _ = _golden_states(case)
+    eng = _engine(cfg, sd)
+    for l in {0, cfg.nlayers - 1}:
+        Xf = feat_sublayer(spec, w, l, X0)
+        got = eng.feature_attention(l, X0.float(), prec).cpu()
+        assert rel_err(got.numpy(), Xf.numpy()) <= TOL[prec], ("feature", l)
+        Xi = item_sublayer(spec, w, l, Xf, N)
+        got = eng.item_attention_block(l, Xf.float(), N, prec).cpu()
+        assert rel_err(got.numpy(), Xi.numpy()) <= TOL[prec], ("item", l)
+        Xm = mlp_sublayer(spec, w, l, Xi)
+        got = eng.mlp_ln(l, Xi.float(), prec).cpu()
+        assert rel_err(got.numpy(), Xm.numpy()) <= TOL[prec], ("mlp", l)
+        X0 = Xm
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("case", ["mgmcap_edge", "mgm_two_mod"])
+def test_mixer_taps_match_oracle(case, prec):
+    z, meta, cfg, sd = load_case(case)
+    spec, w = oracle_spec(cfg), {k: v.double() for k, v in torch_sd(sd).items()}
+    eng = _engine(cfg, sd)
+    im = torch.from_numpy(z["image"])
+    ref = oracle_mgm(spec, w, im.double())
+    got = eng.mgm(im, prec).cpu()
+    assert got.shape == ref.shape
+    assert rel_err(got.numpy(), ref.numpy()) <= 10 * TOL[prec]
+    if cfg.mixer_type == "MGM+CAP":
+        ref_c = oracle_cap(spec, w, ref)
+        got_c = eng.cap(ref.float(), prec).cpu()
+        assert got_c.shape == ref_c.shape
+        assert rel_err(got_c.numpy(), ref_c.numpy()) <= 10 * TOL[prec]
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+def test_taps_at_config_c_shape(prec):
+    """Production shape (S = 2298, N = 1838, T = 36) of each layer tap against the oracle evaluated
+    in fp32 on the same GPU (random O(1) state, layer 0 weights of the config-C model)."""
+    from synth import synth_state_dict
+
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    torch.backends.cuda.matmul.allow_tf32 = False
+    cfg = ModelConfig(nlayers=1, mgm_heads=8, cap_heads=4)
+    sd = synth_state_dict(state_dict_spec(cfg), 2)
+    eng = _engine(cfg, sd)
+    spec, w = oracle_spec(cfg), {k: v.cuda() for k, v in torch_sd(sd).items()}
+    g = torch.Generator(device="cpu").manual_seed(3)
+    X = torch.randn(2298, 36, 192, generator=g).cuda()
+    N = 1838
+    with torch.inference_mode():
+        for name, ref, got in [
+            ("feature", feat_sublayer(spec, w, 0, X), eng.feature_attention(0, X, prec)),
+            ("item", item_sublayer(spec, w, 0, X, N), eng.item_attention_block(0, X, N, prec)),
+            ("mlp", mlp_sublayer(spec, w, 0, X), eng.mlp_ln(0, X, prec)),
+        ]:
+            err = rel_err(got.cpu().numpy(), ref.cpu().numpy())
+            print(f"{name} prec {prec}: rel err {err:.2e}")
+            assert err <= (1e-4 if prec == 0 else TOL[1]), (name, err)
