@@ -427,6 +427,14 @@ __device__ __attribute__((noinline)) void a1_exact_rows(const Attn2Args& p, cons
 #ifndef A2_OCC
 #define A2_OCC (A2_NCH == 2 ? 2 : 3)  // waves per SIMD the register budget targets
 #endif
+// F8: P.V and the row sums on v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 P and V, unit block scales):
+// a measured A/B variant for the long-context config, not the default.  The V^T tile is
+// converted to e4m3 while staged and stored in the k order of the P fragment a lane builds from its
+// S^T accumulators (k = 32 hh + 16 u + r <-> key 32 u + (r & 3) + 8 (r >> 2) + 4 hh), 16-B chunks
+// XOR-swizzled by (d >> 2) & 3; the row sums come from the same instruction with a selector A
+// operand (rows 0 and 4 all ones), so they sum exactly the e4m3 weights the P.V product used.
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+template <bool F8>
 __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args p) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * A2_SPT][2 * 4096];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -501,11 +509,25 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
   };
   const int koff_w = a2_koff(krow, kc);
   const int voff_w0 = a2_voff(vd, vc & ~1) + 8 * (vc & 1), voff_w1 = a2_voff(vd, vc | 1) + 8 * (vc & 1);
+  // F8 V^T image: row vd (64 B), keys vc*8 .. +7 -> logical k 16u + 4q (+32 for the upper 4 keys)
+  const int f8_u = vc >> 2, f8_q = vc & 3;
+  const int f8_off0 = vd * 64 + 16 * ((f8_u) ^ ((vd >> 2) & 3)) + 4 * f8_q;       // k = 16u + 4q, chunk u
+  const int f8_off1 = vd * 64 + 16 * ((2 + f8_u) ^ ((vd >> 2) & 3)) + 4 * f8_q;   // k = 32 + 16u + 4q
   auto lstore = [&](int u, int buf) {
     unsigned char* Ks = lds[buf];
     *(u32x4*)(Ks + koff_w) = rk[u];
-    *(u32x2*)(Ks + 4096 + voff_w0) = u32x2{rv[u].x, rv[u].y};
-    *(u32x2*)(Ks + 4096 + voff_w1) = u32x2{rv[u].z, rv[u].w};
+    if constexpr (F8) {
+      const bf16x8 e = __builtin_bit_cast(bf16x8, rv[u]);
+      int w0 = __builtin_amdgcn_cvt_pk_fp8_f32((float)e[0], (float)e[1], 0, false);
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32((float)e[2], (float)e[3], w0, true);
+      int w1 = __builtin_amdgcn_cvt_pk_fp8_f32((float)e[4], (float)e[5], 0, false);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32((float)e[6], (float)e[7], w1, true);
+      *(int*)(Ks + 4096 + f8_off0) = w0;
+      *(int*)(Ks + 4096 + f8_off1) = w1;
+    } else {
+      *(u32x2*)(Ks + 4096 + voff_w0) = u32x2{rv[u].x, rv[u].y};
+      *(u32x2*)(Ks + 4096 + voff_w1) = u32x2{rv[u].z, rv[u].w};
+    }
   };
   // fragment read offsets (bytes inside a stage)
   int kro[2][2], vro[2][2];
@@ -529,11 +551,22 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 
   f32x16 o[2], negm[2];
   f32x4 lacc[2];
+  f32x16 lacc8[F8 ? 2 : 1];  // F8 row sums: D rows 0 and 4 (lanes 0-31 and 32-63, register 0)
 #pragma unroll
   for (int qb = 0; qb < A2_NCH; ++qb) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[qb][i] = negm[qb][i] = 0.f;
     lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int j = 0; j < (F8 ? 2 : 1); ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lacc8[j][i] = 0.f;
+  i32x8 sel8;  // e4m3 selector: A rows 0 and 4 all ones (0x38 = 1.0)
+  {
+    const int ones = ((lane & 31) == 0 || (lane & 31) == 4) ? 0x38383838 : 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sel8[j] = ones;
   }
 
   auto tile = [&](int it, auto maskc, auto firstc) {
@@ -553,7 +586,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           kf[u][i] = *(const bf16x8*)(Ks + kro[u][i]);
-          vf[u][i] = *(const bf16x8*)(Ks + vro[u][i]);
+          if constexpr (!F8) vf[u][i] = *(const bf16x8*)(Ks + vro[u][i]);
         }
       f32x16 s[2][2];
 #pragma unroll
@@ -594,6 +627,29 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
           }
         }
       }
+      if constexpr (F8) {
+        const unsigned char* Vs8 = Ks + 4096 + r * 64;
+        const int sw = (r >> 2) & 3;
+        const u32x4 v0 = *(const u32x4*)(Vs8 + 16 * ((2 * hh) ^ sw));
+        const u32x4 v1 = *(const u32x4*)(Vs8 + 16 * ((2 * hh + 1) ^ sw));
+        const i32x8 va = i32x8{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+#pragma unroll
+        for (int qb = 0; qb < A2_NCH; ++qb) {
+          i32x8 pf;
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              int x = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_exp2f(s[qb][u][4 * w]),
+                                                      __builtin_amdgcn_exp2f(s[qb][u][4 * w + 1]), 0, false);
+              x = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_exp2f(s[qb][u][4 * w + 2]),
+                                                  __builtin_amdgcn_exp2f(s[qb][u][4 * w + 3]), x, true);
+              pf[4 * u + w] = x;
+            }
+          o[qb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(va, pf, o[qb], 0, 0, 0, 127, 0, 127);
+          lacc8[qb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(sel8, pf, lacc8[qb], 0, 0, 0, 127, 0, 127);
+        }
+      } else
 #pragma unroll
       for (int qb = 0; qb < A2_NCH; ++qb)
 #pragma unroll
@@ -648,8 +704,13 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
   // ---- row sums to the query's lanes, overflow backstop, normalise, store
 #pragma unroll
   for (int qb = 0; qb < A2_NCH; ++qb) {
-    const float a = __shfl(lacc[qb][0], lane & 15, 64), bsum = __shfl(lacc[qb][1], lane & 15, 64);
-    const float ls = r < 16 ? a : bsum;
+    float ls;
+    if constexpr (F8) {
+      ls = lacc8[qb][0];
+    } else {
+      const float a = __shfl(lacc[qb][0], lane & 15, 64), bsum = __shfl(lacc[qb][1], lane & 15, 64);
+      ls = r < 16 ? a : bsum;
+    }
     bf16* orow = p.o + ((int64_t)b * p.S + qsrow[qb]) * (p.H * 32) + qh[qb] * 32;
     // some p overflowed the fixed reference (sum >= 2^100, inf or NaN -- tested on the bits:
     // this file builds with -fno-honor-nans): exact recompute
@@ -695,7 +756,11 @@ hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void*
   a.tasks_per_b = acc;
   a.nblocks = acc * T;
   if (a.nblocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(attn_item2_kernel, dim3(a.nblocks), dim3(256), 0, st, a);
+#ifdef MMPFN_ATTN_FP8PV
+  hipLaunchKernelGGL(attn_item2_kernel<true>, dim3(a.nblocks), dim3(256), 0, st, a);
+#else
+  hipLaunchKernelGGL(attn_item2_kernel<false>, dim3(a.nblocks), dim3(256), 0, st, a);
+#endif
   return hipGetLastError();
 }
 

@@ -12,7 +12,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 from multimodalpfn_amd import _lib  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
-T, H, d, S, N = int(os.environ.get("ATT_T", 36)), 6, 32, 2298, 1838
+T, H, d = int(os.environ.get("ATT_T", 36)), 6, 32
+S, N = int(os.environ.get("ATT_S", 2298)), int(os.environ.get("ATT_N", 1838))
 Npad = (N + 63) // 64 * 64
 lib = _lib.load_library(os.environ.get("MMPFN_LIB") or None)
 ctx = lib.mmpfn_create(0, None)
