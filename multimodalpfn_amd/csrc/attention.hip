@@ -437,7 +437,8 @@ typedef __attribute__((ext_vector_type(8))) int i32x8;
 template <bool F8>
 __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args p) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * A2_SPT][2 * 4096];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar task / activity tests
   const int r = lane & 31, hh = lane >> 5;
 
   // ---- task: contiguous task ranges per XCD (blocks of one KV sequence share an L2)
