@@ -304,55 +304,75 @@ class HipEngine:
 
         Members are spread over ``lanes`` forward lanes (per-member workspaces of the same
         context), each on its own HIP stream, so one member's kernels fill the tails and
-        latency gaps of another's.  The caller's stream waits for all of them.  The
-        reference runs its members one after another (inference.py:294-349); the results
-        do not depend on the lane count.
+        latency gaps of another's; members of one geometry are stacked ``batch`` at a time
+        into one batched forward.  ``items`` may be a generator: a unit is launched as soon as
+        its members have arrived, so the caller's host work for later members (the per-member
+        preprocessing of a predict) overlaps the GPU work of earlier ones.  The caller's stream
+        waits for all of them.  The reference runs its members one after another
+        (inference.py:294-349); the results do not depend on lanes or batching.
         """
-        items = list(items)
         batch = max(1, int(self.batch if batch is None else batch))
-        # work units: batches of up to `batch` members of one geometry, in member order
-        groups: dict = {}
-        for i, (x, t, y) in enumerate(items):
-            groups.setdefault(self._geometry(x, t, y), []).append(i)
-        units = []
-        for idx in groups.values():
-            units += [idx[j:j + batch] for j in range(0, len(idx), batch)]
-        units.sort(key=lambda u: u[0])
-        if lanes is None:
-            lanes = self.lanes
-        lanes = max(1, min(int(lanes), len(units), _lib.MMPFN_MAX_LANES))
-        outs: list = [None] * len(items)
+        if isinstance(items, (list, tuple)):
+            n_units = len({self._geometry(*it) for it in items})  # lower bound on the unit count
+            n_units = max(n_units, -(-len(items) // batch))
+        else:
+            n_units = _lib.MMPFN_MAX_LANES
+        lanes = max(1, min(int(self.lanes if lanes is None else lanes), n_units, _lib.MMPFN_MAX_LANES))
+        outs: dict[int, torch.Tensor] = {}
+        store: dict[int, tuple] = {}
 
         def run(unit):
             if len(unit) == 1:
-                x, t, y = items[unit[0]]
+                x, t, y = store[unit[0]]
                 outs[unit[0]] = self.forward(x, t, y, precision, check_nan=False)
             else:
-                for i, o in zip(unit, self.forward_batch([items[i] for i in unit], precision)):
+                for i, o in zip(unit, self.forward_batch([store[i] for i in unit], precision)):
                     outs[i] = o
+            for i in unit:
+                del store[i]
 
-        if lanes == 1:
-            for u in units:
-                run(u)
-            return outs
         main = torch.cuda.current_stream(self.device)
-        streams = self._lane_streams(lanes)
-        for st in streams:
-            st.wait_stream(main)
-        try:
-            for k, u in enumerate(units):
-                with torch.cuda.stream(streams[k % lanes]):
-                    self._check(self.lib.mmpfn_select_lane(self.ctx, k % lanes), "mmpfn_select_lane")
-                    run(u)
+        streams = self._lane_streams(lanes) if lanes > 1 else [main]
+        if lanes > 1:
+            for st in streams:
+                st.wait_stream(main)
+        launched = 0
+
+        def launch(unit):
+            nonlocal launched
+            if lanes == 1:
+                run(unit)
+            else:
+                k = launched % lanes
+                with torch.cuda.stream(streams[k]):
+                    self._check(self.lib.mmpfn_select_lane(self.ctx, k), "mmpfn_select_lane")
+                    run(unit)
                     if _DEBUG_SYNC:
                         torch.cuda.synchronize(self.device)
+            launched += 1
+
+        pending: dict = {}  # geometry -> member indices waiting for a full unit
+        n = 0
+        try:
+            for i, it in enumerate(items):
+                n = i + 1
+                store[i] = it
+                g = self._geometry(*it)
+                pending.setdefault(g, []).append(i)
+                if len(pending[g]) == batch:
+                    launch(pending.pop(g))
+            for unit in sorted(pending.values(), key=lambda u: u[0]):
+                launch(unit)
         finally:
-            self._check(self.lib.mmpfn_select_lane(self.ctx, 0), "mmpfn_select_lane")
-            for st in streams:
-                main.wait_stream(st)
-        for o in outs:  # allocated on a lane stream, consumed on the caller's
-            o.record_stream(main)
-        return outs
+            if lanes > 1:
+                self._check(self.lib.mmpfn_select_lane(self.ctx, 0), "mmpfn_select_lane")
+                for st in streams:
+                    main.wait_stream(st)
+        result = [outs[i] for i in range(n)]
+        if lanes > 1:
+            for o in result:  # allocated on a lane stream, consumed on the caller's
+                o.record_stream(main)
+        return result
 
     def _geometry(self, x, tokens, y_train) -> tuple:
         S = (x.shape[0] if x is not None else tokens.shape[0])

@@ -37,12 +37,23 @@ def _precision(model, device: torch.device, autocast: bool, forced: torch.dtype 
     return _lib.PREC_BF16 if (autocast and device.type == "cuda") else _lib.PREC_F32
 
 
-def _mixer_tokens(model, eng, image_train, image_test, prec: int):
-    """Shared modality tokens of all members (``transformer.py:560-600``), or None."""
+def _mixer_tokens(model, eng, image_train, image_test, prec: int, cache: dict | None = None):
+    """Shared modality tokens of all members (``transformer.py:560-600``), or None.
+
+    The projection heads are row-wise (MGM: per-row LN + gated MLP; CAP: each row's queries
+    attend that row's MGM tokens; MoE: per-row gate and experts), so the train rows' tokens do
+    not depend on the test rows: with ``cache`` they are computed at the first predict and kept
+    on the device, and every predict projects only its test rows."""
     if image_train is None or image_test is None or model.mixer_type not in ("MGM", "MGM+CAP", "MoE"):
         return None
-    img = np.concatenate([np.asarray(image_train, dtype=np.float32), np.asarray(image_test, dtype=np.float32)], 0)
-    return eng.mixer_tokens(torch.from_numpy(img), prec)
+    test = eng.mixer_tokens(torch.from_numpy(np.asarray(image_test, dtype=np.float32)), prec)
+    key = ("train_tokens", str(eng.device), prec)
+    train = None if cache is None else cache.get(key)
+    if train is None:
+        train = eng.mixer_tokens(torch.from_numpy(np.asarray(image_train, dtype=np.float32)), prec)
+        if cache is not None:
+            cache[key] = train
+    return torch.cat([train, test], 0)
 
 
 @dataclass
@@ -60,6 +71,9 @@ class InferenceEngine:
 
     save_peak_mem: bool | Literal["auto"] | float | int
     dtype_byte_size: int
+    # device copies of what every predict re-uses: the train rows' modality tokens and each
+    # member's preprocessed train table (the reference re-uploads both per member and predict)
+    _device_cache: dict = field(default_factory=dict, repr=False)
 
     def iter_outputs(self, X, image_test, *, device: torch.device, autocast: bool) -> Iterator[tuple]:
         raise NotImplementedError
@@ -72,22 +86,30 @@ class InferenceEngine:
         eng = model.engine(model._device() if device.type != "cuda" else device)
         prec = _precision(model, eng.device, autocast, forced_dtype)
         mine, gather = member_shard(len(members), [self._member_cost(m, X, image_test) for m in members])
-        tokens = _mixer_tokens(model, eng, image_train, image_test, prec) if mine else None
-        items = []
-        for i in mine:
-            m = members[i]
-            if m.X_train is not None:
-                X_test = m.preprocessor.transform(X).X
-                x_full = np.concatenate([np.asarray(m.X_train, np.float32), np.asarray(X_test, np.float32)], 0)
-            else:
+        cache = self._device_cache if self._cacheable else None
+        tokens = _mixer_tokens(model, eng, image_train, image_test, prec, cache) if mine else None
+        def items():  # a generator: forward_many launches each unit as soon as its members are ready
+            for i in mine:
+                m = members[i]
                 x_full = None
-            items.append((None if x_full is None else torch.from_numpy(x_full), tokens,
-                          np.asarray(m.y_train, np.float32)))
-        outs: dict[int, torch.Tensor] = dict(zip(mine, eng.forward_many(items, prec)))
+                if m.X_train is not None:
+                    X_test = torch.from_numpy(np.asarray(m.preprocessor.transform(X).X, np.float32)).to(eng.device)
+                    key = ("X_train", i, str(eng.device))
+                    xtr = None if cache is None else cache.get(key)
+                    if xtr is None:
+                        xtr = torch.from_numpy(np.asarray(m.X_train, np.float32)).to(eng.device)
+                        if cache is not None:
+                            cache[key] = xtr
+                    x_full = torch.cat([xtr, X_test], 0)
+                yield x_full, tokens, np.asarray(m.y_train, np.float32)
+
+        outs: dict[int, torch.Tensor] = dict(zip(mine, eng.forward_many(items(), prec)))
         if mine:
             eng.status()  # NaN / HIP errors of every queued member (transformer.py:727-731,790-796)
         Q = len(X) if X is not None else len(image_test)
         return gather(outs, eng.device, Q, model.cfg.n_out)
+
+    _cacheable = True  # the members' train tables and train images are fixed after fit
 
     @staticmethod
     def _member_cost(m: _Member, X, image_test) -> float:
@@ -135,6 +157,8 @@ class InferenceEngineCachePreprocessing(InferenceEngine):
 @dataclass
 class InferenceEngineOnDemand(InferenceEngine):
     """Nothing cached: members' preprocessing re-fitted at every predict (``inference.py:73-213``)."""
+
+    _cacheable = False
 
     X_train: np.ndarray | None = None
     y_train: np.ndarray | None = None
