@@ -19,7 +19,8 @@ flops 4*T*Nq*Nk*E per launch; every launch of a separate pass of the same steps
 bracketed by HIP events on its lane stream, mmpfn_kernel_timing), ``f32_parity_mode``
 (the same step in the fp32 parity mode), ``config_D`` (image + text, 32 members),
 ``api_end_to_end`` (MMPFNClassifier.predict_proba from host numpy, PCIe-inclusive),
-``kv_cache_predict`` (fit_with_cache serving) and ``cpu_baseline`` /
+``kv_cache_predict`` (fit_with_cache serving), ``modality_encoders`` (the DINOv2 / ELECTRA
+towers that produce the image tokens) and ``cpu_baseline`` /
 ``cpu_baseline_einsum`` (the oracle's CPU restatement of the same forward in the
 reference's two attention branches, on the host cores, one member).
 """
@@ -62,6 +63,8 @@ def parse():
     p.add_argument("--api-steps", type=int, default=3, help="timed predict_proba calls of the API leg (0: skip)")
     p.add_argument("--no-kv-cache", dest="kv_cache", action="store_false", help="skip the fit_with_cache leg")
     p.add_argument("--no-config-d", dest="config_d", action="store_false", help="skip the config-D leg")
+    p.add_argument("--no-modality", dest="modality", action="store_false",
+                   help="skip the modality-encoder leg (DINOv2 ViT-B/14, ELECTRA-base)")
     p.add_argument("--no-f32", dest="f32_leg", action="store_false", help="skip the fp32 parity-mode leg")
     p.add_argument("--no-cpu-einsum", dest="cpu_einsum", action="store_false",
                    help="skip the einsum-branch CPU baseline (the SDPA branch always runs)")
@@ -398,6 +401,66 @@ def config_d_leg(device, world, rank, args, prec):
     }
 
 
+def vit_flops(B, H, W, D=768, depth=12, P=14, cls_only=True) -> float:
+    """Executed flops of DINOv2 ViT-B/14 forward_features (the last block on the CLS rows only)."""
+    np_ = (H // P) * (W // P)
+    L = 1 + np_
+    f = 2.0 * B * np_ * (3 * P * P) * D  # patch embedding
+    full = 2.0 * L * D * 3 * D + 4.0 * L * L * D + 2.0 * L * D * D + 2.0 * 2 * L * D * 4 * D
+    tail = 2.0 * L * D * 3 * D + 4.0 * L * D + 2.0 * D * D + 2.0 * 2 * D * 4 * D
+    return f + B * ((depth - 1) * full + (tail if cls_only else full))
+
+
+def modality_leg(device, args):
+    """the image tower the reference runs once per dataset (pad_ufes_20.py:66-107):
+    DINOv2 ViT-B/14 x_norm_clstoken of 336 x 336 images (the reference's img_size 14 * 24), and the
+    ELECTRA-base text tower (petfinder.py:150-181), random-init weights of those architectures."""
+    from modality_cases import text_config, text_state, vit_state
+
+    from multimodalpfn_amd.modality import ElectraTextEncoder, vit_base
+
+    out = {}
+    c = dict(dim=768, depth=12, heads=12, patch=14, img_size=518, init_values=1.0, offset=0.1, seed=31)
+    m = vit_base(patch_size=14, img_size=518, init_values=1.0, num_register_tokens=0, block_chunks=0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in vit_state(c).items()})
+    B, H = 128, 336
+    x = torch.rand((B, 3, H, H), generator=torch.Generator().manual_seed(5)).to(device)
+    for prec in ("bf16", "f32"):
+        m.precision = prec
+        m.cls_embeddings(x)
+        torch.cuda.synchronize(device)
+        k = 5 if prec == "bf16" else 2
+        t0 = time.perf_counter()
+        for _ in range(k):
+            m.cls_embeddings(x)
+        torch.cuda.synchronize(device)
+        dt = (time.perf_counter() - t0) / k
+        fl = vit_flops(B, H, H)
+        out["vit_b14_" + prec] = {"value": round(B / dt, 1), "unit": "images/s", "ms_per_batch": round(dt * 1e3, 2),
+                                  "batch": B, "image": f"{H}x{H}", "tflops": round(fl / dt / 1e12, 1),
+                                  "frac_of_bf16_peak": round(fl / dt / 1e12 / BF16_PEAK_TFLOPS, 4)}
+    m._drop_contexts()
+    tc = dict(vocab=30522, emb=768, dim=768, depth=12, heads=12, ffn=3072, max_pos=512, types=2, seed=32)
+    t = ElectraTextEncoder(text_config(tc), precision="bf16")
+    t.load_state_dict({k: torch.from_numpy(v) for k, v in text_state(tc).items()})
+    Bt, Lt = 256, 128
+    ids = torch.randint(1, 30522, (Bt, Lt), generator=torch.Generator().manual_seed(6)).to(device)
+    mask = torch.ones_like(ids)
+    t.cls_embeddings(ids, mask)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        t.cls_embeddings(ids, mask)
+    torch.cuda.synchronize(device)
+    dt = (time.perf_counter() - t0) / 5
+    out["electra_base_bf16"] = {"value": round(Bt / dt, 1), "unit": "texts/s", "ms_per_batch": round(dt * 1e3, 2),
+                                "batch": Bt, "tokens": Lt}
+    t._drop_contexts()
+    out["note"] = ("random-init weights of the reference's towers (the pretrained checkpoints are not available "
+                   "offline); executed flops with the last block on the CLS rows only")
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -479,6 +542,12 @@ def main():
             roof["other_configs_isolated_launch"][name] = {k: r[k] for k in ("achieved", "frac", "per_launch_ms")}
     eng.close()
     cfg_d = config_d_leg(device, world, rank, args, prec) if args.config_d else None
+    mod = None
+    if args.modality and rank == 0:
+        try:
+            mod = modality_leg(device, args)
+        except Exception as e:  # noqa: BLE001 - reported, the headline number stands on its own
+            mod = {"error": f"{type(e).__name__}: {e}"}
     cpu = cpu_e = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sd, x, y, image, use_sdpa=True)
@@ -526,6 +595,7 @@ def main():
             "f32_parity_mode": f32,
             "config_D": cfg_d,
             "kv_cache_predict": kv,
+            "modality_encoders": mod,
         }
         print(json.dumps(line))
     if world > 1:

@@ -86,6 +86,43 @@ SIGNATURES = [
                                       ctypes.POINTER(ctypes.c_double)]),
 ]
 
+# include/mmpfn_modality.h (modality encoders: DINOv2 ViT, ELECTRA text tower)
+MMPFN_ENC_VIT = 1
+MMPFN_ENC_TEXT = 2
+
+
+class EncDesc(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int),
+        ("dim", ctypes.c_int),
+        ("depth", ctypes.c_int),
+        ("heads", ctypes.c_int),
+        ("mlp_hidden", ctypes.c_int),
+        ("ln_eps", ctypes.c_float),
+        ("patch", ctypes.c_int),
+        ("in_chans", ctypes.c_int),
+        ("pos_grid", ctypes.c_int),
+        ("interp_offset", ctypes.c_double),
+        ("layerscale", ctypes.c_int),
+        ("vocab", ctypes.c_int),
+        ("max_pos", ctypes.c_int),
+        ("type_vocab", ctypes.c_int),
+        ("embedding_size", ctypes.c_int),
+    ]
+
+
+MODALITY_SIGNATURES = [
+    ("mmpfn_enc_create", _vp, [_i, _vp]),
+    ("mmpfn_enc_destroy", None, [_vp]),
+    ("mmpfn_enc_last_error", ctypes.c_char_p, [_vp]),
+    ("mmpfn_enc_set_stream", _i, [_vp, _vp]),
+    ("mmpfn_enc_set_model", _i, [_vp, ctypes.POINTER(EncDesc)]),
+    ("mmpfn_enc_load_weight", _i, [_vp, ctypes.c_char_p, _vp, _i64]),
+    ("mmpfn_enc_finalize", _i, [_vp]),
+    ("mmpfn_vit_forward", _i, [_vp, _vp, _i, _i, _i, _vp, _vp, _i]),
+    ("mmpfn_text_forward", _i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _i]),
+]
+
 _LIB = None
 
 
@@ -105,7 +142,7 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     import torch  # noqa: F401
 
     lib = ctypes.CDLL(str(p))
-    for name, res, args in SIGNATURES:
+    for name, res, args in SIGNATURES + MODALITY_SIGNATURES:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -124,5 +161,16 @@ def check(lib, ctx, rc: int, what: str) -> None:
     msg = lib.mmpfn_last_error(ctx)
     msg = msg.decode() if msg else ""
     if rc == MMPFN_ERR_NAN:
+        raise ValueError(f"{what}: {msg}")
+    raise EngineError(f"{what} failed (rc={rc}): {msg}")
+
+
+def check_enc(lib, enc, rc: int, what: str) -> None:
+    """Status of a modality-encoder call (include/mmpfn_modality.h)."""
+    if rc == MMPFN_OK:
+        return
+    msg = lib.mmpfn_enc_last_error(enc)
+    msg = msg.decode() if msg else ""
+    if rc == MMPFN_ERR_INVALID:
         raise ValueError(f"{what}: {msg}")
     raise EngineError(f"{what} failed (rc={rc}): {msg}")

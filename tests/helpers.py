@@ -14,7 +14,7 @@ from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
 from oracle.forward import OracleSpec
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
-CASES = sorted(p.stem for p in GOLDEN.glob("*.npz") if not p.stem.startswith("api_"))
+CASES = sorted(p.stem for p in GOLDEN.glob("*.npz") if not p.stem.startswith(("api_", "modality_")))
 
 
 def load_case(name: str):

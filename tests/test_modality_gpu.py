@@ -1,0 +1,141 @@
+"""Modality encoders on the device against the reference's golden vectors:
+DINOv2 ViT ``forward_features`` (reference vit_base code) and transformers' ``ElectraModel``, seeded
+random weights (tests/golden/make_modality_golden.py).
+
+Tolerances (rel = max |d| / max(1, max |ref|)):
+  fp32 mode (the reference's arithmetic): <= 1e-4;
+  bf16 mode (bf16 MFMA operands, fp32 accumulate / residual / LN / softmax): the band written per
+  case below, about twice the deviation measured on MI355X (printed by each test).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from modality_cases import TEXT_CASES, VIT_CASES, text_config, text_inputs, text_state, vit_images, vit_state
+from multimodalpfn_amd.modality import DinoVisionTransformer, ElectraTextEncoder, embed_images
+
+pytestmark = pytest.mark.gpu
+
+GOLD = __import__("pathlib").Path(__file__).resolve().parent / "golden"
+F32_TOL = 1e-4
+# measured on MI355X (max over cls / tokens): vit_small_img 5.8e-3, vit_336 5.6e-3, vit_rect_nols 4.3e-3,
+# electra_base 9.7e-3, electra_proj_masked 4.4e-3
+BF16_TOL = {"vit_small_img": 1.2e-2, "vit_336": 1.2e-2, "vit_rect_nols": 1e-2, "electra_base": 2e-2,
+            "electra_proj_masked": 1e-2}
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(1.0, np.abs(b).max()))
+
+
+_VIT: dict = {}
+
+
+def vit_model(name):
+    if name not in _VIT:
+        c = VIT_CASES[name]
+        m = DinoVisionTransformer(img_size=c["img_size"], patch_size=c["patch"], embed_dim=c["dim"], depth=c["depth"],
+                                  num_heads=c["heads"], init_values=c["init_values"], block_chunks=0,
+                                  interpolate_offset=c["offset"])
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in vit_state(c).items()})
+        _VIT.clear()
+        _VIT[name] = m
+    return _VIT[name]
+
+
+@pytest.mark.parametrize("name", sorted(VIT_CASES))
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+def test_vit_forward_features_matches_reference(name, prec):
+    c = VIT_CASES[name]
+    g = np.load(GOLD / f"modality_{name}.npz")
+    m = vit_model(name)
+    m.precision = prec
+    x = torch.from_numpy(vit_images(c)).cuda()
+    out = m.forward_features(x)
+    cls = out["x_norm_clstoken"].cpu().numpy()
+    keep = g["patch_tokens"].shape[1]
+    pt = out["x_norm_patchtokens"][:, :keep].cpu().numpy()
+    e_cls, e_tok = rel(cls, g["cls"]), rel(pt, g["patch_tokens"])
+    print(f"{name} {prec}: cls rel {e_cls:.3e}, patch tokens rel {e_tok:.3e}")
+    tol = F32_TOL if prec == "f32" else BF16_TOL[name]
+    assert e_cls <= tol and e_tok <= tol
+    # the CLS-only path (last block on the CLS rows) gives the same embedding
+    fast = m.cls_embeddings(x).cpu().numpy()
+    if prec == "f32":
+        assert np.array_equal(fast, cls)
+    else:
+        assert rel(fast, cls) < 1e-3
+
+
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+def test_vit_batch_rows_are_independent(prec):
+    """Each image's embedding does not depend on the batch it is computed in (bitwise)."""
+    c = VIT_CASES["vit_rect_nols"]
+    m = vit_model("vit_rect_nols")
+    m.precision = prec
+    x = torch.from_numpy(vit_images(c)).cuda()
+    full = m.cls_embeddings(x)
+    for i in range(x.shape[0]):
+        assert torch.equal(m.cls_embeddings(x[i:i + 1]), full[i:i + 1])
+
+
+def test_embed_images_mirrors_reference_loop():
+    """pad_ufes_20.py:86-103: [N, n_img, C, H, W] in batches -> [N, n_img, D]."""
+    c = VIT_CASES["vit_rect_nols"]
+    m = vit_model("vit_rect_nols")
+    m.precision = "f32"
+    imgs = torch.from_numpy(vit_images(c))  # [3, 3, 42, 70]
+    stacked = torch.stack([imgs, imgs.flip(0)], 1)  # N = 3 rows, 2 images each
+    emb = embed_images(m, stacked, batch_size=2)
+    assert emb.shape == (3, 2, 768)
+    ref = m.cls_embeddings(imgs.cuda()).cpu()
+    assert torch.equal(emb[:, 0], ref) and torch.equal(emb[:, 1], ref.flip(0))
+
+
+def text_model(name):
+    c = TEXT_CASES[name]
+    m = ElectraTextEncoder(text_config(c))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in text_state(c).items()})
+    return m
+
+
+@pytest.mark.parametrize("name", sorted(TEXT_CASES))
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+def test_electra_matches_reference(name, prec):
+    c = TEXT_CASES[name]
+    g = np.load(GOLD / f"modality_{name}.npz")
+    m = text_model(name)
+    m.precision = prec
+    ids, types = text_inputs(c)
+    tol = F32_TOL if prec == "f32" else BF16_TOL[name]
+    errs = []
+    for j, (t, tt) in enumerate(zip(ids, types)):  # one text per call, like the reference
+        h = m(torch.from_numpy(t)[None].cuda(), torch.ones(1, len(t), dtype=torch.long).cuda(),
+              torch.from_numpy(tt)[None].cuda()).last_hidden_state[0].cpu().numpy()
+        errs.append(rel(h, g[f"hidden_{j}"]))
+    # the padded batch under attention_mask: the real tokens match the per-text runs
+    L = max(len(t) for t in ids)
+    bid = torch.zeros((len(ids), L), dtype=torch.long)
+    bm = torch.zeros_like(bid)
+    btt = torch.zeros_like(bid)
+    for j, (t, tt) in enumerate(zip(ids, types)):
+        bid[j, :len(t)], bm[j, :len(t)], btt[j, :len(t)] = torch.from_numpy(t), 1, torch.from_numpy(tt)
+    hb = m(bid.cuda(), bm.cuda(), btt.cuda()).last_hidden_state.cpu().numpy()
+    for j, t in enumerate(ids):
+        errs.append(rel(hb[j, :len(t)], g[f"hidden_{j}"]))
+    print(f"{name} {prec}: rel {max(errs):.3e}")
+    assert max(errs) <= tol
+    cls = m.cls_embeddings(bid.cuda(), bm.cuda(), btt.cuda()).cpu().numpy()
+    if prec == "f32":
+        assert np.array_equal(cls, hb[:, 0])
+    else:
+        assert rel(cls, hb[:, 0]) < 2e-3
+
+
+def test_electra_out_of_range_ids_raise():
+    m = text_model("electra_proj_masked")
+    with pytest.raises(IndexError):
+        m(torch.tensor([[1, 2, 5000]]).cuda())
