@@ -425,7 +425,7 @@ __device__ __attribute__((noinline)) void a1_exact_rows(const Attn2Args& p, cons
 }
 
 #ifndef A2_OCC
-#define A2_OCC (A2_NCH == 2 ? 2 : 3)  // waves per SIMD the register budget targets
+#define A2_OCC (A2_NCH == 4 ? 1 : A2_NCH == 2 ? 2 : 3)  // waves per SIMD the register budget targets
 #endif
 // F8: P.V and the row sums on v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 P and V, unit block scales):
 // a measured A/B variant for the long-context config, not the default.  The V^T tile is
@@ -466,9 +466,9 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
   const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
 
   // ---- the lane's query of each 32-query chain
-  int qh[2], qsrow[2];
-  bool qok[2];
-  bf16x8 qf[2][2];
+  int qh[A2_NCH], qsrow[A2_NCH];
+  bool qok[A2_NCH];
+  bf16x8 qf[A2_NCH][2];
 #pragma unroll
   for (int qb = 0; qb < A2_NCH; ++qb) {
     const int j = jw + 32 * qb + r;
@@ -550,9 +550,9 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     for (int j = 0; j < 8; ++j) sel[j] = (bf16)(one ? 1.0f : 0.0f);
   }
 
-  f32x16 o[2], negm[2];
-  f32x4 lacc[2];
-  f32x16 lacc8[F8 ? 2 : 1];  // F8 row sums: D rows 0 and 4 (lanes 0-31 and 32-63, register 0)
+  f32x16 o[A2_NCH], negm[A2_NCH];
+  f32x4 lacc[A2_NCH];
+  f32x16 lacc8[F8 ? A2_NCH : 1];  // F8 row sums: D rows 0 and 4 (lanes 0-31 and 32-63, register 0)
 #pragma unroll
   for (int qb = 0; qb < A2_NCH; ++qb) {
 #pragma unroll
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
-  for (int j = 0; j < (F8 ? 2 : 1); ++j)
+  for (int j = 0; j < (F8 ? A2_NCH : 1); ++j)
 #pragma unroll
     for (int i = 0; i < 16; ++i) lacc8[j][i] = 0.f;
   i32x8 sel8;  // e4m3 selector: A rows 0 and 4 all ones (0x38 = 1.0)
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
           kf[u][i] = *(const bf16x8*)(Ks + kro[u][i]);
           if constexpr (!F8) vf[u][i] = *(const bf16x8*)(Ks + vro[u][i]);
         }
-      f32x16 s[2][2];
+      f32x16 s[A2_NCH][2];
 #pragma unroll
       for (int qb = 0; qb < A2_NCH; ++qb)
 #pragma unroll
