@@ -37,6 +37,11 @@ def _precision(model, device: torch.device, autocast: bool, forced: torch.dtype 
     return _lib.PREC_BF16 if (autocast and device.type == "cuda") else _lib.PREC_F32
 
 
+def _h2d(a, device: torch.device) -> torch.Tensor:
+    """fp32 host array -> device on the current stream."""
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(device)
+
+
 def _mixer_tokens(model, eng, image_train, image_test, prec: int, cache: dict | None = None):
     """Shared modality tokens of all members (``transformer.py:560-600``), or None.
 
@@ -46,7 +51,12 @@ def _mixer_tokens(model, eng, image_train, image_test, prec: int, cache: dict | 
     on the device, and every predict projects only its test rows."""
     if image_train is None or image_test is None or model.mixer_type not in ("MGM", "MGM+CAP", "MoE"):
         return None
-    test = eng.mixer_tokens(torch.from_numpy(np.asarray(image_test, dtype=np.float32)), prec)
+    # the test image rows (1.4 MB at PAD-UFES size) through pinned memory, asynchronously on the stream
+    # the mixer runs on (a pageable copy is staged by the runtime in host-synchronous chunks)
+    img = torch.from_numpy(np.ascontiguousarray(image_test, dtype=np.float32))
+    if eng.device.type == "cuda":
+        img = img.pin_memory().to(eng.device, non_blocking=True)
+    test = eng.mixer_tokens(img, prec)
     key = ("train_tokens", str(eng.device), prec)
     train = None if cache is None else cache.get(key)
     if train is None:
@@ -93,11 +103,11 @@ class InferenceEngine:
                 m = members[i]
                 x_full = None
                 if m.X_train is not None:
-                    X_test = torch.from_numpy(np.asarray(m.preprocessor.transform(X).X, np.float32)).to(eng.device)
+                    X_test = _h2d(m.preprocessor.transform(X).X, eng.device)
                     key = ("X_train", i, str(eng.device))
                     xtr = None if cache is None else cache.get(key)
                     if xtr is None:
-                        xtr = torch.from_numpy(np.asarray(m.X_train, np.float32)).to(eng.device)
+                        xtr = _h2d(m.X_train, eng.device)
                         if cache is not None:
                             cache[key] = xtr
                     x_full = torch.cat([xtr, X_test], 0)
