@@ -373,6 +373,13 @@ constexpr int A2_NW = 4;
 #ifndef A2_SPT
 #define A2_SPT 1  // 64-key tiles per LDS stage (one barrier per stage)
 #endif
+#ifndef A2_AHEAD
+#define A2_AHEAD 1  // tiles in flight ahead of the one computed (2: two staging register sets, A2_SPT == 1)
+#endif
+#ifndef A2_NOMAX_DIAG
+#define A2_NOMAX_DIAG 0  // diagnostics only: reference max 0 (no first-tile max), wrong for large scores
+#endif
+static_assert(A2_AHEAD == 1 || A2_SPT == 1, "prefetch depth 2 needs one tile per stage");
 constexpr int A2_QPW = 32 * A2_NCH;  // queries per wave
 constexpr int A2_QPB = A2_NW * A2_QPW;
 
@@ -434,12 +441,20 @@ __device__ __attribute__((noinline)) void a1_exact_rows(const Attn2Args& p, cons
 // XOR-swizzled by (d >> 2) & 3; the row sums come from the same instruction with a selector A
 // operand (rows 0 and 4 all ones), so they sum exactly the e4m3 weights the P.V product used.
 typedef __attribute__((ext_vector_type(8))) int i32x8;
+#ifdef A2_STAMPS  // diagnostics build: per-block timeline (tools/attn_stamps.py)
+__device__ unsigned long long a2_stamp_buf[16384 * 6];
+#define A2_STAMP(i) \
+  if (tid == 0 && blockIdx.x < 16384) a2_stamp_buf[blockIdx.x * 6 + (i)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define A2_STAMP(i)
+#endif
 template <bool F8>
 __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args p) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * A2_SPT][2 * 4096];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar task / activity tests
   const int r = lane & 31, hh = lane >> 5;
+  A2_STAMP(0);
 
   // ---- task: contiguous task ranges per XCD (blocks of one KV sequence share an L2)
   int b, g, chunk;
@@ -495,7 +510,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
   // ---- staging: one 16-B K chunk and one 16-B V^T chunk per thread and tile
   const int krow = tid >> 2, kc = tid & 3;      // K tile [64][32]: row, chunk
   const int vd = tid >> 3, vc = tid & 7;        // V^T tile [32][64]: row d, natural 8-key chunk
-  u32x4 rk[A2_SPT], rv[A2_SPT];
+  u32x4 rk[A2_SPT * A2_AHEAD], rv[A2_SPT * A2_AHEAD];
   auto gload = [&](int u, int t) {  // tile t into staging registers u
     const int k0 = t * A2_KT;
     rk[u] = *(const u32x4*)(Kg + (int64_t)(k0 + krow) * 32 + kc * 8);
@@ -570,16 +585,22 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     for (int j = 0; j < 8; ++j) sel8[j] = ones;
   }
 
-  auto tile = [&](int it, auto maskc, auto firstc) {
+  auto tile = [&](int it, auto maskc, auto firstc, auto parc) {
     constexpr bool MASK = decltype(maskc)::value;
     constexpr bool FIRST = decltype(firstc)::value;
+    constexpr int PAR = decltype(parc)::value;  // it & 1 (A2_AHEAD == 2: the staging set / LDS slot)
     const int k0 = it * A2_KT;
     const int sub = it % A2_SPT;  // position inside the stage of A2_SPT tiles
+#if A2_AHEAD == 2
+    if (it + 2 < ntiles) gload(PAR, it + 2);  // set PAR held tile it, staged at the last barrier
+    const unsigned char* Ks = lds[PAR];
+#else
     if (sub == 0)
 #pragma unroll
       for (int u = 0; u < A2_SPT; ++u)
         if (it + A2_SPT + u < ntiles) gload(u, it + A2_SPT + u);
     const unsigned char* Ks = lds[it % (2 * A2_SPT)];
+#endif
     if (active) {
       bf16x8 kf[2][2], vf[2][2];
 #pragma unroll
@@ -612,7 +633,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
             for (int i = 0; i < 16; ++i)
               if (k0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * hh >= p.nk) s[qb][u][i] = -INFINITY;
       }
-      if constexpr (FIRST) {  // fix the reference max per query: this tile's row max
+      if constexpr (FIRST && !A2_NOMAX_DIAG) {  // fix the reference max per query: this tile's row max
 #pragma unroll
         for (int qb = 0; qb < A2_NCH; ++qb) {
           float m = fmaxf(s[qb][0][0], s[qb][1][0]);
@@ -676,30 +697,64 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 #endif
           }
     }
+#if A2_AHEAD == 2
+    // tile it+1 (loaded a tile ago) goes to the slot tile it-1 used: every wave left it at the last barrier
+    if (it + 1 < ntiles) lstore(PAR ^ 1, PAR ^ 1);
+    __syncthreads();
+    (void)sub;
+#else
+    (void)PAR;
     if (sub == A2_SPT - 1) {  // end of a stage: the next stage's tiles go to the other half of the ring
 #pragma unroll
       for (int u = 0; u < A2_SPT; ++u)
         if (it + 1 + u < ntiles) lstore(u, (it + 1 + u) % (2 * A2_SPT));
       __syncthreads();
     }
+#endif
   };
 
+#if A2_AHEAD == 2
+  gload(0, 0);
+  if (ntiles > 1) gload(1, 1);
+  lstore(0, 0);
+#else
 #pragma unroll
   for (int u = 0; u < A2_SPT; ++u)
     if (u < ntiles) gload(u, u);
 #pragma unroll
   for (int u = 0; u < A2_SPT; ++u)
     if (u < ntiles) lstore(u, u);
+#endif
   __syncthreads();
+  A2_STAMP(1);
+  using P0 = std::integral_constant<int, 0>;
+  using P1 [[maybe_unused]] = std::integral_constant<int, 1>;
+  using Y = std::true_type;
+  using N = std::false_type;
   if (ntiles == 1) {
-    if (partial) tile(0, std::true_type{}, std::true_type{});
-    else tile(0, std::false_type{}, std::true_type{});
+    if (partial) tile(0, Y{}, Y{}, P0{});
+    else tile(0, N{}, Y{}, P0{});
   } else {
-    tile(0, std::false_type{}, std::true_type{});
+    tile(0, N{}, Y{}, P0{});
+    A2_STAMP(2);
     const int nfull = p.nk / A2_KT;
-    for (int it = 1; it < nfull; ++it) tile(it, std::false_type{}, std::false_type{});
-    if (partial) tile(nfull, std::true_type{}, std::false_type{});
+#if A2_AHEAD == 2
+    int it = 1;
+    for (; it + 1 < nfull; it += 2) {
+      tile(it, N{}, N{}, P1{});
+      tile(it + 1, N{}, N{}, P0{});
+    }
+    if (it < nfull) tile(it++, N{}, N{}, P1{});
+    if (partial) {
+      if (it & 1) tile(it, Y{}, N{}, P1{});
+      else tile(it, Y{}, N{}, P0{});
+    }
+#else
+    for (int it = 1; it < nfull; ++it) tile(it, N{}, N{}, P0{});
+    if (partial) tile(nfull, Y{}, N{}, P0{});
+#endif
   }
+  A2_STAMP(3);
   if (!active) return;
 
   // ---- row sums to the query's lanes, overflow backstop, normalise, store
@@ -732,9 +787,19 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
       }
     }
   }
+#ifdef A2_STAMPS
+  A2_STAMP(4);
+  if (tid == 0 && blockIdx.x < 16384) a2_stamp_buf[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
 }
 
 }  // namespace
+
+#ifdef A2_STAMPS
+extern "C" int mmpfn_dbg_attn_stamps(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(a2_stamp_buf), sizeof(a2_stamp_buf));
+}
+#endif
 
 hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride) {

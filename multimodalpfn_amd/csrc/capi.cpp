@@ -644,9 +644,9 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
       HIPCHK(launch_attn_item(Qi, Kc, Vc, O, S, TM, H, cc->Npad, 0, S, cc->N, 0, prec, st, cstride));
   } else {
     if (bf && E == 192) {  // row-resident projections straight into the attention layouts
-      HIPCHK(launch_rowgemm_qkv(Xall, N, S, 1, 0, L.item_qkv_h.p, TM * N, 3 * E, Qi, Ki, Vi, S, Npad, H, st));
-      if (Q > 0)
-        HIPCHK(launch_rowgemm_qkv(Xall, Q, S, 1, N, L.item_qtest_h.p, TM * Q, E, Qi, Ki, Vi, S, Npad, H, st));
+      // train rows q|k|v and test rows q in one launch (test-row blocks last)
+      HIPCHK(launch_rowgemm_qkv_pair(Xall, N, 0, L.item_qkv_h.p, TM * N, 3 * E, Q, N, L.item_qtest_h.p, TM * Q, E, S,
+                                     Qi, Ki, Vi, S, Npad, H, st));
     } else {
       GemmArgs a = gargs();
       a.A = Xall, a.lda = E, a.a_rdiv = N, a.a_rmul = S, a.a_roff = 0;

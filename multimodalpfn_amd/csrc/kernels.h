@@ -74,6 +74,11 @@ hipError_t launch_mlp_rows(float* X, const void* W1perm, const void* W2perm, int
 hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
                               const void* W, int M, int N, void* q, void* k, void* vt, int S, int Npad, int H,
                               hipStream_t st);
+// two row sets (train rows: q|k|v, test rows: q) of the same token columns in ONE launch,
+// rows m -> memory row (m / rdiv) * a_rmul + m % rdiv + roff of each set
+hipError_t launch_rowgemm_qkv_pair(const float* X, int64_t rdiv1, int64_t roff1, const void* W1, int M1, int N1,
+                                   int64_t rdiv2, int64_t roff2, const void* W2, int M2, int N2, int64_t a_rmul,
+                                   void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st);
 // C = (ln ? LayerNorm(A) : A) . W^T + bias: A fp32 [M][192], W [N][192] bf16, C bf16 [M][N], N % 64 == 0
 hipError_t launch_rowgemm_ln_store(const float* A, const void* W, const float* bias, void* C, int64_t M, int N,
                                    float eps, bool ln, hipStream_t st);

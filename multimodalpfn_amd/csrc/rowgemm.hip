@@ -165,13 +165,12 @@ constexpr int OVST = 32 + 8;    // V^T tile row stride (bf16): 80 B
 constexpr int OWEL = QC * OVST; // per-wave staging elements (>= 32 * OQST)
 static_assert(32 * OQST <= OWEL, "Q/K staging tile must fit");
 
-__global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p, int tiles_per_b) {
-  __shared__ __attribute__((aligned(16))) bf16 Ws[2 * QCEL + 4 * OWEL];
+__device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int bid, bf16* Ws) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int rd = (int)p.a_rdiv;
-  const int b = blockIdx.x / tiles_per_b;
-  const int l0 = (blockIdx.x - b * tiles_per_b) * GROWS + wave * 32;  // wave's first row inside column b
+  const int b = bid / tiles_per_b;
+  const int l0 = (bid - b * tiles_per_b) * GROWS + wave * 32;  // wave's first row inside column b
   bf16* const Os = Ws + 2 * QCEL + wave * OWEL;
   const int nch = p.N / QC;
   u32x4 r[QCP];
@@ -283,6 +282,16 @@ __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p, in
     __syncthreads();
 #endif
   }
+}
+
+// Two row sets in one launch: blocks [0, nblk1) project p's rows (the train rows: q|k|v), the
+// rest p2's (the test rows: q only, a third of the chunks) -- the short test-row blocks run last
+// and fill the grid's tail instead of a separate under-filled launch.
+__global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p, int tiles_per_b, const RgArgs p2,
+                                                              int tiles2, int nblk1) {
+  __shared__ __attribute__((aligned(16))) bf16 Ws[2 * QCEL + 4 * OWEL];
+  if ((int)blockIdx.x < nblk1) qkv2_tile(p, tiles_per_b, blockIdx.x, Ws);
+  else qkv2_tile(p2, tiles2, blockIdx.x - nblk1, Ws);
 }
 
 // C[m] = (LN? LayerNorm(A[m]) : A[m]) . W^T + bias, A fp32 [M][192], W [N][192] bf16, C bf16 [M][N]
@@ -438,21 +447,52 @@ __global__ __launch_bounds__(256, 2) void rowgemm_resln_kernel(const RgArgs p) {
 
 }  // namespace
 
-hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
-                              const void* W, int M, int N, void* q, void* k, void* vt, int S, int Npad, int H,
-                              hipStream_t st) {
+namespace {
+// one row set of the QKV projection: args, row tiles per column and block count (0 blocks: M == 0)
+hipError_t qkv_rowset(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff, const void* W,
+                      int M, int N, void* q, void* k, void* vt, int S, int Npad, int H, RgArgs& a, int& tiles,
+                      int64_t& nblk) {
+  a = RgArgs{};
+  tiles = 1, nblk = 0;
   if (M <= 0) return hipSuccess;
   if ((N != GE && N != 3 * GE) || H * 32 != GE) return hipErrorInvalidValue;
-  RgArgs a{};
   a.A = X, a.a_rdiv = a_rdiv, a.a_rmul = a_rmul, a.a_rmul2 = a_rmul2, a.a_roff = a_roff;
   a.W = (const bf16*)W, a.M = M, a.N = N;
   a.q = (bf16*)q, a.k = (bf16*)k, a.vt = (bf16*)vt, a.S = S, a.Npad = Npad, a.H = H;
   // blocks tile each column b separately: nb = M / a_rdiv columns of a_rdiv rows
   if (a_rdiv <= 0 || M % a_rdiv != 0) return hipErrorInvalidValue;
   if (N == 3 * GE && (a_roff % 8 != 0 || a_roff + a_rdiv > Npad)) return hipErrorInvalidValue;  // 16-B V^T stores
-  const int tiles = (int)((a_rdiv + GROWS - 1) / GROWS);
-  const int64_t nblk = (int64_t)tiles * (M / a_rdiv);
-  hipLaunchKernelGGL(rowgemm_qkv2_kernel, dim3((unsigned)nblk), dim3(256), 0, st, a, tiles);
+  tiles = (int)((a_rdiv + GROWS - 1) / GROWS);
+  nblk = (int64_t)tiles * (M / a_rdiv);
+  return hipSuccess;
+}
+}  // namespace
+
+hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
+                              const void* W, int M, int N, void* q, void* k, void* vt, int S, int Npad, int H,
+                              hipStream_t st) {
+  RgArgs a;
+  int tiles;
+  int64_t nblk;
+  hipError_t e = qkv_rowset(X, a_rdiv, a_rmul, a_rmul2, a_roff, W, M, N, q, k, vt, S, Npad, H, a, tiles, nblk);
+  if (e != hipSuccess || nblk == 0) return e;
+  hipLaunchKernelGGL(rowgemm_qkv2_kernel, dim3((unsigned)nblk), dim3(256), 0, st, a, tiles, a, tiles, (int)nblk);
+  return hipGetLastError();
+}
+
+hipError_t launch_rowgemm_qkv_pair(const float* X, int64_t rdiv1, int64_t roff1, const void* W1, int M1, int N1,
+                                   int64_t rdiv2, int64_t roff2, const void* W2, int M2, int N2, int64_t a_rmul,
+                                   void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st) {
+  RgArgs a1, a2;
+  int t1, t2;
+  int64_t n1, n2;
+  hipError_t e = qkv_rowset(X, rdiv1, a_rmul, 1, roff1, W1, M1, N1, q, k, vt, S, Npad, H, a1, t1, n1);
+  if (e != hipSuccess) return e;
+  e = qkv_rowset(X, rdiv2, a_rmul, 1, roff2, W2, M2, N2, q, k, vt, S, Npad, H, a2, t2, n2);
+  if (e != hipSuccess) return e;
+  if (n1 + n2 == 0) return hipSuccess;
+  if (n1 == 0) a1 = a2, t1 = t2;  // blocks index the second set only
+  hipLaunchKernelGGL(rowgemm_qkv2_kernel, dim3((unsigned)(n1 + n2)), dim3(256), 0, st, a1, t1, a2, t2, (int)n1);
   return hipGetLastError();
 }
 
