@@ -499,13 +499,33 @@ def main():
 
     # ---- live roofline of the dominant kernel: a SEPARATE pass of the same steps with every
     #      attention launch bracketed by HIP events on its lane stream (kept out of the headline)
-    eng.lib.mmpfn_kernel_timing(eng.ctx, 1)
-    dt_live = timed_steps(step, args.steps, 0, world, device)
-    eng.lib.mmpfn_kernel_timing(eng.ctx, 0)
+    #      Two such passes: the headline's own lane setting (launches share the CUs with the other
+    #      lane's kernels, so their event durations are not the kernel's), and one lane (the same
+    #      batched launch shape, kernels one after another): the kernel's own duration, the primary
+    #      figure, which `rocprofv3 --kernel-trace -- bench.py --lanes 1` reproduces.
     batch = eng.batch if args.batch is None else args.batch
-    live = live_roofline(eng.lib, eng.ctx, T * min(batch, len(mine))) if rank == 0 else None
-    if live is not None:
-        live["timing"] += f"; a separate pass of {args.steps} steps ({dt_live / args.steps * 1e3:.3f} ms per step)"
+    lanes = eng.lanes if args.lanes is None else args.lanes
+    T_launch = T * min(batch, len(mine))
+
+    def live_pass(stp):
+        eng.lib.mmpfn_kernel_timing(eng.ctx, 1)
+        dt_l = timed_steps(stp, args.steps, 1, world, device)
+        eng.lib.mmpfn_kernel_timing(eng.ctx, 0)
+        r = live_roofline(eng.lib, eng.ctx, T_launch) if rank == 0 else None
+        if r is not None:
+            r["timing"] += f"; a separate pass of {args.steps} steps ({dt_l / args.steps * 1e3:.3f} ms per step)"
+        return r
+
+    live_ovl = live_pass(step)
+    live = live_ovl
+    if lanes > 1:
+        step_l1 = make_step(eng, members, mine, assignment, rank, img, prec, 1, args.batch)
+        live = live_pass(step_l1)
+        if live is not None:
+            live["timing"] = live["timing"].replace(
+                "lanes overlap, so a launch shares the GPU with the other lane's kernels",
+                "one lane: launches run one after another, as in `bench.py --lanes 1`")
+            live["in_step_overlapped"] = {k: live_ovl[k] for k in ("achieved", "frac", "per_launch_ms", "timing")}
 
     # ---- the fp32 parity mode (what the 1e-4 logits contract costs)
     f32 = None

@@ -13,12 +13,12 @@
 //     permuted (pos 8g+j <-> hidden 4g+j / 16+4g+j-4; W2 stored so, capi.cpp pack_mlp2_perm);
 //   * the 192 x 32 output accumulator Y^T, initialised with the fp32 residual itself (X, or the
 //     fused prologue's X'), so the residual never leaves registers; then LayerNorm across lanes.
-// Software pipeline over hidden chunks c (branch-free body, last chunk peeled): GELU(H(c)) on
-// the VALU beside the MFMAs of H(c+1), then Y^T += W2c . GELU(H(c)); one barrier per chunk.
-// Only the weights move through LDS: a 128-row block (4 waves) shares each chunk; W1 of chunk
-// c+2 and W2 of chunk c+1 are loaded into registers during chunk c and written to their LDS
-// slots after it (two slots each, 62 KB per block: two blocks per CU).  LDS rows of 416 B
-// (W1) and 96 B (W2) keep the ds_read_b128 fragment reads conflict-free.
+// Software pipeline over hidden chunks c: GELU(H(c)) on the VALU beside the MFMAs of H(c+1), then
+// Y^T += W2c . GELU(H(c)); one barrier per chunk.  Only the weights move through LDS: a 128-row block
+// (4 waves) shares each chunk, delivered by LDS-DMA into three-slot W1 / W2 rings (72 KB per block,
+// two blocks per CU) two chunks ahead of use, unpadded and XOR-swizzled (see the ring comment below).
+// Measured against register staging into two padded slots (in-step launch, rocprofv3): 168-171 ->
+// 162-163 us per two-member launch; a DMA ring whose peeled tail chunks spilled 130 VGPRs ran 197 us.
 #include "common.h"
 #include "kernels.h"
 
@@ -28,12 +28,20 @@ namespace {
 
 constexpr int RE = 192;                    // model width
 constexpr int RHC = 32;                    // hidden chunk
-constexpr int W1ST = RE + 16;              // W1 chunk LDS row stride (bf16): 416 B
-constexpr int W2ST = RHC + 16;             // W2 chunk LDS row stride (bf16): 96 B
-constexpr int W1EL = RHC * W1ST;           // 6656
-constexpr int W2EL = RE * W2ST;            // 9216
-constexpr int P1 = RHC * RE / 8 / 256;     // 16-B W1 pieces per thread and chunk (3)
-constexpr int P2 = RE * RHC / 8 / 256;     // 16-B W2 pieces per thread and chunk (3)
+constexpr int W1ST = RE + 16;              // RES Wout staging row stride (bf16): 416 B
+constexpr int SLOT_B = RHC * RE * 2;       // one W1 or W2 chunk image: 12 KB
+constexpr int NSLOT = 3;                   // ring depth per matrix
+constexpr int W2RING = NSLOT * SLOT_B;     // byte offset of the W2 ring
+constexpr int LDS_B = 2 * NSLOT * SLOT_B;  // 72 KB per block: two blocks per CU
+constexpr int MP = SLOT_B / 1024 / 4;      // 1-KB DMA pieces per wave, matrix and chunk (3)
+constexpr int WOUT_E = 2 * SLOT_B / 2;     // RES: Wout staging (bf16 offset) over W1 slot 2 and the W2 ring
+typedef __attribute__((ext_vector_type(2))) float float2_t;
+
+__device__ __forceinline__ void mlp_dma16(uint32_t voff, const void* sbase, unsigned lds_dst) {
+  // m0 = the wave's LDS destination; lane i's 16 B (sbase + voff) land at m0 + 16 i
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_dst)
+               : "memory");
+}
 
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -49,45 +57,56 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
                                                                        float eps, const bf16* __restrict__ O,
                                                                        const bf16* __restrict__ Wout) {
   constexpr int RROWS = 4 * 16 * TT;  // rows per block
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * W1EL + 2 * W2EL];
-  bf16* const w1s = lds;
-  bf16* const w2s = lds + 2 * W1EL;
+  __shared__ __attribute__((aligned(1024))) bf16 lds[LDS_B / 2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * RROWS + wave * 16 * TT;
   const int nchunks = Fh / RHC;
 
-  // register staging: piece p of W1 chunk c = row c*32 + p/24, 16-B column p%24;
-  // piece q of W2 chunk c = row q/4, 16-B column q%4 of the chunk's 32 permuted columns
-  u32x4 r1[P1], r2[P2];
-  auto fetch1 = [&](int c) {
+  // Weight rings filled by LDS-DMA (global_load_lds_dwordx4 in inline asm, so the compiler adds no
+  // vmcnt(0) before reads of the other slots; the kernel waits for its own pieces explicitly): three
+  // W1 slots (chunk c+1 read by this chunk's up-projection, c+2 landing, c+3 in flight) and three W2
+  // slots (chunk c read, c+1 landing, c+2 in flight), so every fill has two chunks to arrive.  Images
+  // are unpadded with 16-B units XOR-swizzled for conflict-free ds_read_b128 fragment reads:
+  //   W1 slot [32 rows][384 B]: unit u of row r at (u ^ ((r >> 1) & 7))
+  // (conflict-free for ds_read_b128's four lane groups, MI355X_MICROARCH.md LDS table)
+  //   W2 slot [192 rows][64 B]: unit u of row r at (u ^ ((r >> 2) & 2))
+  // The DMA writes lane-linearly (lane i of a wave instruction -> 16 i of its 1-KB piece), so each
+  // lane fetches the unit that belongs at its position: a per-lane 32-bit offset from a uniform
+  // chunk base (saddr form), three pieces per wave and matrix per chunk.
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
+  uint32_t o1[MP], o2[MP];
 #pragma unroll
-    for (int j = 0; j < P1; ++j) {
-      const int p = tid + 256 * j;
-      r1[j] = *(const u32x4*)(W1 + (int64_t)(c * RHC + p / 24) * RE + (p % 24) * 8);
-    }
-  };
-  auto fetch2 = [&](int c) {
+  for (int j = 0; j < MP; ++j) {
+    const int q = (wave * MP + j) * 64 + lane;  // unit index inside a slot image
+    const int r1 = q / 24, u1 = (q % 24) ^ ((r1 >> 1) & 7);
+    o1[j] = (uint32_t)(r1 * RE + u1 * 8) * 2;
+    const int r2 = q >> 2, u2 = (q & 3) ^ ((r2 >> 2) & 2);
+    o2[j] = (uint32_t)(r2 * Fh + u2 * 8) * 2;
+  }
+  auto dma_w1 = [&](int c, int slot) {  // W1 rows c*32 .. +31
+    const bf16* base = W1 + (int64_t)c * RHC * RE;
 #pragma unroll
-    for (int j = 0; j < P2; ++j) {
-      const int q = tid + 256 * j;
-      r2[j] = *(const u32x4*)(W2p + (int64_t)(q >> 2) * Fh + c * RHC + (q & 3) * 8);
-    }
+    for (int j = 0; j < MP; ++j)
+      mlp_dma16(o1[j], base, __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT_B + (wave * MP + j) * 1024));
   };
-  auto stash1 = [&](int slot) {
+  auto dma_w2 = [&](int c, int slot) {  // W2 columns c*32 .. +31 (permuted), all 192 rows
+    const bf16* base = W2p + c * RHC;
 #pragma unroll
-    for (int j = 0; j < P1; ++j) {
-      const int p = tid + 256 * j;
-      *(u32x4*)(w1s + slot * W1EL + (p / 24) * W1ST + (p % 24) * 8) = r1[j];
-    }
+    for (int j = 0; j < MP; ++j)
+      mlp_dma16(o2[j], base,
+                __builtin_amdgcn_readfirstlane(lds0 + W2RING + slot * SLOT_B + (wave * MP + j) * 1024));
   };
-  auto stash2 = [&](int slot) {
-#pragma unroll
-    for (int j = 0; j < P2; ++j) {
-      const int q = tid + 256 * j;
-      *(u32x4*)(w2s + slot * W2EL + (q >> 2) * W2ST + (q & 3) * 8) = r2[j];
-    }
-  };
+  // fragment read offsets (bytes inside a slot): W1 row 16 ht + fr, unit 4 ks + fg; W2 row 16 o + fr, unit fg
+  const int s1 = (fr >> 1) & 7;
+  const uint32_t f1e = fr * 384 + ((fg ^ s1) << 4), f1o = fr * 384 + (((4 + fg) ^ s1) << 4);
+  const uint32_t f2 = W2RING + fr * 64 + ((fg ^ ((fr >> 2) & 2)) << 4);
+  const unsigned char* ldsb = (const unsigned char*)lds;
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  dma_w1(0, 0);  // under the prologue (W1 slots 0-1 are outside the Wout staging)
+  if (nchunks > 1) dma_w1(1, 1);
 
   // ---- the wave's rows as B fragments in the Y^T lane layout: lane (row 16tt + fr, group fg)
   //      holds features 16f + 4fg + i; K position 32ks + 8fg + j <-> feature of tile f = 2ks + j/4
@@ -130,7 +149,7 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
 #pragma unroll
         for (int j = 0; j < PC / 3; ++j) {
           const int pc = tid + 256 * (r * (PC / 3) + j);
-          *(u32x4*)(lds + (pc / 24) * W1ST + (pc % 24) * 8) = st[j];
+          *(u32x4*)(lds + WOUT_E + (pc / 24) * W1ST + (pc % 24) * 8) = st[j];
         }
       }
       __syncthreads();
@@ -138,7 +157,7 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
       for (int ks = 0; ks < RE / 32; ++ks)
 #pragma unroll
         for (int fl = 0; fl < 6; ++fl) {
-          const bf16x8 w = *(const bf16x8*)(lds + (fl * 16 + fr) * W1ST + ks * 32 + fg * 8);
+          const bf16x8 w = *(const bf16x8*)(lds + WOUT_E + (fl * 16 + fr) * W1ST + ks * 32 + fg * 8);
 #pragma unroll
           for (int tt = 0; tt < TT; ++tt) y[6 * half + fl][tt] = mfma16(w, ao[tt][ks], y[6 * half + fl][tt]);
         }
@@ -176,11 +195,7 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
         for (int i = 0; i < 4; ++i) y[f][tt][i] = (y[f][tt][i] - mean) * inv;
       to_af(tt);
     }
-    fetch1(0);
-    fetch2(0);
   } else {
-    fetch1(0);
-    fetch2(0);
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
       const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
@@ -190,16 +205,22 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
       to_af(tt);
     }
   }
-  stash1(0);
-  stash2(0);
-  if (nchunks > 1) {
-    fetch1(1);
-    stash1(1);
-  }
+  // (W1 slot 2 and the W2 ring held the RES prologue's Wout staging until its last barrier)
+  dma_w2(0, 0);
+  if (nchunks > 2) dma_w1(2, 2);
+  if (nchunks > 1) dma_w2(1, 1);
+  // before chunk 0: W1(0), W1(1) and W2(0) landed; W1(2) and W2(1) (needed by its end) may fly
+  if (nchunks > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * MP) : "memory");
+  else if (nchunks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MP) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // H^T [32 hidden][16 TT rows] = W1c . A^T  (W1c in LDS)
-  auto hmma = [&](const bf16* w1, f32x4 (&h)[2][TT]) {
+  // H^T [32 hidden][16 TT rows] = W1c . A^T  (W1c in W1 slot SL)
+  auto hmma = [&](auto slc, f32x4 (&h)[2][TT]) {
+    constexpr int SL = decltype(slc)::value;
+    auto w1frag = [&](int ht, int ks) {
+      return *(const bf16x8*)(ldsb + SL * SLOT_B + ht * 16 * 384 + (ks >> 1) * 128 + ((ks & 1) ? f1o : f1e));
+    };
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -209,7 +230,7 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
 #pragma unroll
     for (int i = 0; i < PU; ++i)
 #pragma unroll
-      for (int ht = 0; ht < 2; ++ht) wa[i][ht] = *(const bf16x8*)(w1 + (ht * 16 + fr) * W1ST + i * 32 + fg * 8);
+      for (int ht = 0; ht < 2; ++ht) wa[i][ht] = w1frag(ht, i);
 #pragma unroll
     for (int ks = 0; ks < RE / 32; ++ks) {
       __builtin_amdgcn_sched_barrier(0);
@@ -219,69 +240,80 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
         for (int tt = 0; tt < TT; ++tt) h[ht][tt] = mfma16(wa[ks % PU][ht], af[tt][ks], h[ht][tt]);
       if (ks + PU < RE / 32)
 #pragma unroll
-        for (int ht = 0; ht < 2; ++ht)
-          wa[ks % PU][ht] = *(const bf16x8*)(w1 + (ht * 16 + fr) * W1ST + (ks + PU) * 32 + fg * 8);
+        for (int ht = 0; ht < 2; ++ht) wa[ks % PU][ht] = w1frag(ht, ks + PU);
     }
   };
   // y holds the residual (X, or X' after the fused prologue) in fp32: the down-projection MFMAs
   // accumulate onto it, so the residual is never written out and read back
   f32x4 h[2][TT];
-  hmma(w1s, h);
-  // chunk 0 overwrites W1 slot 0 (with W1(2)) after its MFMAs: every wave of the block must have
-  // finished reading slot 0 above first -- without this barrier a wave that lags a whole chunk
-  // behind (another kernel sharing its SIMD) read half-replaced W1(0) fragments
-  if (nchunks > 2) __syncthreads();
+  hmma(S0{}, h);
+  // chunk 0 refills W1 slot 0 (with W1(3)): every wave of the block must have finished reading it
+  // first (a wave can lag a whole chunk behind when another kernel shares its SIMD)
+  if (nchunks > 3) __syncthreads();
 
-  // one chunk: slots W1(c+1) in w1s[(c+1)&1], W2(c) in w2s[c&1]; W1(c+2) -> w1s[c&1] and
-  // W2(c+1) -> w2s[(c+1)&1], written after this chunk's reads; both slots were last read in
-  // chunk c-1 (or, for W1(0), right before chunk 0, behind the barrier after that read)
-  auto chunk = [&](int c, auto morec) {
-    constexpr bool MORE = decltype(morec)::value;  // a chunk c+1 exists
+  // one chunk c (PAR = c % 3): reads W1(c+1) from W1 slot (c+1)%3 and W2(c) from W2 slot c%3;
+  // refills W1 slot c%3 (W1(c), read in chunk c-1) with W1(c+3) and W2 slot (c+2)%3 (W2(c-1)) with
+  // W2(c+2); at its end W1(c+2) and W2(c+1), issued a chunk earlier, must have landed
+  auto chunk = [&](int c, auto parc) {
+    const bool MORE = c + 1 < nchunks;  // a chunk c+1 exists (wave-uniform)
+    constexpr int PAR = decltype(parc)::value;
+    [[maybe_unused]] const bool d1 = c + 3 < nchunks, d2 = c + 2 < nchunks;
 #ifndef MLP_NOSTAGE
-    const bool f1 = c + 2 < nchunks;
-    if (f1) fetch1(c + 2);
-    if (MORE) fetch2(c + 1);
+    if (d1) dma_w1(c + 3, PAR);
+    if (d2) dma_w2(c + 2, (PAR + 2) % 3);
 #endif
     bf16x8 hb[TT];  // GELU of chunk c (VALU) beside the up-projection MFMAs of chunk c+1
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {  // adjacent pairs: one v_cvt_pk_bf16_f32 each
 #ifndef MLP_NOGELU
-        hb[tt][i] = (bf16)gelu_tanh_fast(h[0][tt][i]);
-        hb[tt][4 + i] = (bf16)gelu_tanh_fast(h[1][tt][i]);
-#else
-        hb[tt][i] = (bf16)h[0][tt][i];
-        hb[tt][4 + i] = (bf16)h[1][tt][i];
+          const bf16x2 pr = __builtin_convertvector(
+              (float2_t){gelu_tanh_fast(h[ht][tt][i]), gelu_tanh_fast(h[ht][tt][i + 1])}, bf16x2);
+#else  // ablation: identity activation
+          const bf16x2 pr = __builtin_convertvector((float2_t){h[ht][tt][i], h[ht][tt][i + 1]}, bf16x2);
 #endif
-      }
+          hb[tt][4 * ht + i] = pr[0];
+          hb[tt][4 * ht + i + 1] = pr[1];
+        }
     }
-    if (MORE) hmma(w1s + ((c + 1) & 1) * W1EL, h);
+    if (MORE) hmma(std::integral_constant<int, (PAR + 1) % 3>{}, h);
     // Y^T [192][32 rows] += W2c(perm) . GELU(H^T)
-    const bf16* w2 = w2s + (c & 1) * W2EL;
     {  // W2 fragments 4 tiles ahead of their MFMAs (fenced so the reads stay early; 3-6 measured)
       constexpr int PF = 4;
+      auto w2frag = [&](int o) { return *(const bf16x8*)(ldsb + PAR * SLOT_B + o * 16 * 64 + f2); };
       bf16x8 wb[PF];
 #pragma unroll
-      for (int i = 0; i < PF; ++i) wb[i] = *(const bf16x8*)(w2 + (i * 16 + fr) * W2ST + fg * 8);
+      for (int i = 0; i < PF; ++i) wb[i] = w2frag(i);
 #pragma unroll
       for (int o = 0; o < RE / 16; ++o) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int tt = 0; tt < TT; ++tt) y[o][tt] = mfma16(wb[o % PF], hb[tt], y[o][tt]);
-        if (o + PF < RE / 16) wb[o % PF] = *(const bf16x8*)(w2 + ((o + PF) * 16 + fr) * W2ST + fg * 8);
+        if (o + PF < RE / 16) wb[o % PF] = w2frag(o + PF);
       }
     }
+    if (MORE) {
 #ifndef MLP_NOSTAGE
-    if (f1) stash1(c & 1);
-    if (MORE) stash2((c + 1) & 1);
+      // this thread's pieces of W1(c+2) and W2(c+1) landed; this chunk's own fills may still fly
+      if (d1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * MP) : "memory");
+      else if (d2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MP) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
 #ifndef MLP_NOSYNC
-    __syncthreads();
+      __syncthreads();
 #endif
+    }
   };
-  for (int c = 0; c + 1 < nchunks; ++c) chunk(c, std::true_type{});
-  chunk(nchunks - 1, std::false_type{});
+  // unrolled by three so that every ring slot is a compile-time offset (no peeled copies: the last
+  // chunk's "no successor" is a uniform branch)
+  for (int c = 0; c < nchunks; c += 3) {
+    chunk(c, S0{});
+    if (c + 1 < nchunks) chunk(c + 1, S1{});
+    if (c + 2 < nchunks) chunk(c + 2, S2{});
+  }
 
   // residual + LayerNorm: lane = row, 48 of its 192 features (rows 16o + 4g + i of Y^T)
 #pragma unroll
