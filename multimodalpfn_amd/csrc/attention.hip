@@ -351,13 +351,17 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
 // Per 64-key tile and wave: 8 x v_mfma_f32_32x32x16_bf16 for S^T = K Q^T (query on the
 // lane), 8 for O^T += V^T P^T, 8 x v_mfma_f32_16x16x32_bf16 that sum P^T rows through a
 // 0/1 selector operand (the row sum never touches the VALU), 64 v_exp_f32 + 32 cvt_pk per
-// lane.  The softmax reference is FIXED after the first tile: m = that tile's row max, the
-// S^T chains start from the accumulator -m, p = exp2(s - m) feeds the MFMA unchanged.  No
-// per-tile max, no rescale.  Scaling by a power of two is exact, so the result equals the
-// running-max form up to rounding as long as no p overflows; p <= 2^100 is checked once at
-// the end (the row sum bounds every p) and a wave that fails it recomputes its queries with
-// an exact two-pass softmax (a1_exact_rows) -- a numerical backstop for score jumps of more
-// than ~88 (natural-log units) past the first tile's max, never taken on model data.
+// lane.  The softmax reference is FIXED: the first pass uses m = 0 (p = exp2(s) straight from the
+// S^T accumulator -- no max, no subtraction, every tile alike), the row sum l is checked once at
+// the end against [2^-60, 2^100) (it bounds every p from above, and p_max >= l / N from below), and
+// a block in which any query leaves that range re-runs its tile loop with m = the first tile's row
+// max, the S^T chains starting from the accumulator -m.  Scaling by a power of two is exact, so
+// either pass equals the running-max softmax up to rounding; keys more than ~60 below the row max
+// (log2 units) may flush to zero, 2^-60 of the max and less.  A wave whose second pass still
+// overflows (a score ~88 natural-log units past the first tile's max) recomputes its queries with
+// an exact two-pass softmax (a1_exact_rows).  Neither fallback is taken on model data; the
+// reference-free pass removes the first tile's max / subtract / reference moves (setup + first tile
+// 5.06 -> 4.07 us of a 37-us block at config C, -DA2_STAMPS).
 //
 // LDS images (no padding, XOR-swizzled 16-B chunks; conflict-free ds_read_b128 for the
 // four 16-lane groups of a wave, MI355X_MICROARCH.md LDS table):
@@ -375,9 +379,6 @@ constexpr int A2_NW = 4;
 #endif
 #ifndef A2_AHEAD
 #define A2_AHEAD 1  // tiles in flight ahead of the one computed (2: two staging register sets, A2_SPT == 1)
-#endif
-#ifndef A2_NOMAX_DIAG
-#define A2_NOMAX_DIAG 0  // diagnostics only: reference max 0 (no first-tile max), wrong for large scores
 #endif
 static_assert(A2_AHEAD == 1 || A2_SPT == 1, "prefetch depth 2 needs one tile per stage");
 constexpr int A2_QPW = 32 * A2_NCH;  // queries per wave
@@ -633,7 +634,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
             for (int i = 0; i < 16; ++i)
               if (k0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * hh >= p.nk) s[qb][u][i] = -INFINITY;
       }
-      if constexpr (FIRST && !A2_NOMAX_DIAG) {  // fix the reference max per query: this tile's row max
+      if constexpr (FIRST) {  // fix the reference max per query: this tile's row max (second pass)
 #pragma unroll
         for (int qb = 0; qb < A2_NCH; ++qb) {
           float m = fmaxf(s[qb][0][0], s[qb][1][0]);
@@ -731,42 +732,88 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
   using P1 [[maybe_unused]] = std::integral_constant<int, 1>;
   using Y = std::true_type;
   using N = std::false_type;
-  if (ntiles == 1) {
-    if (partial) tile(0, Y{}, Y{}, P0{});
-    else tile(0, N{}, Y{}, P0{});
-  } else {
-    tile(0, N{}, Y{}, P0{});
-    A2_STAMP(2);
-    const int nfull = p.nk / A2_KT;
+  // one pass over the key tiles; WM: the first tile fixes the reference (row max), else m = 0
+  auto pass = [&](auto wmc) {
+    constexpr bool WM = decltype(wmc)::value;
+    using F = std::integral_constant<bool, WM>;
+    if (ntiles == 1) {
+      if (partial) tile(0, Y{}, F{}, P0{});
+      else tile(0, N{}, F{}, P0{});
+    } else {
+      tile(0, N{}, F{}, P0{});
+      A2_STAMP(2);
+      const int nfull = p.nk / A2_KT;
 #if A2_AHEAD == 2
-    int it = 1;
-    for (; it + 1 < nfull; it += 2) {
-      tile(it, N{}, N{}, P1{});
-      tile(it + 1, N{}, N{}, P0{});
-    }
-    if (it < nfull) tile(it++, N{}, N{}, P1{});
-    if (partial) {
-      if (it & 1) tile(it, Y{}, N{}, P1{});
-      else tile(it, Y{}, N{}, P0{});
-    }
+      int it = 1;
+      for (; it + 1 < nfull; it += 2) {
+        tile(it, N{}, N{}, P1{});
+        tile(it + 1, N{}, N{}, P0{});
+      }
+      if (it < nfull) tile(it++, N{}, N{}, P1{});
+      if (partial) {
+        if (it & 1) tile(it, Y{}, N{}, P1{});
+        else tile(it, Y{}, N{}, P0{});
+      }
 #else
-    for (int it = 1; it < nfull; ++it) tile(it, N{}, N{}, P0{});
-    if (partial) tile(nfull, Y{}, N{}, P0{});
+      for (int it = 1; it < nfull; ++it) tile(it, N{}, N{}, P0{});
+      if (partial) tile(nfull, Y{}, N{}, P0{});
 #endif
-  }
+    }
+  };
+  // the row sum of chain qb on the query's lanes
+  auto rowsum = [&](int qb) {
+    if constexpr (F8) {
+      return lacc8[qb][0];
+    } else {
+      const float a = __shfl(lacc[qb][0], lane & 15, 64), bsum = __shfl(lacc[qb][1], lane & 15, 64);
+      return r < 16 ? a : bsum;
+    }
+  };
+  pass(N{});
   A2_STAMP(3);
+  {  // reference-free pass out of range ([2^-60, 2^100), tested on the bits; this file builds with
+     // -fno-honor-nans) for any query of the block: all waves re-run with the first tile's max
+    bool bad = false;
+    if (active)
+#pragma unroll
+      for (int qb = 0; qb < A2_NCH; ++qb) {
+        const unsigned lb = __float_as_uint(rowsum(qb)) & 0x7fffffffu;
+        bad |= lb >= 0x71800000u || lb < 0x21800000u;
+      }
+    const int any_bad = __syncthreads_or(bad ? 1 : 0);
+    if (any_bad) {
+#pragma unroll
+      for (int qb = 0; qb < A2_NCH; ++qb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[qb][i] = negm[qb][i] = 0.f;
+        lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int j = 0; j < (F8 ? A2_NCH : 1); ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lacc8[j][i] = 0.f;
+#if A2_AHEAD == 2
+      gload(0, 0);
+      if (ntiles > 1) gload(1, 1);
+      lstore(0, 0);
+#else
+#pragma unroll
+      for (int u = 0; u < A2_SPT; ++u)
+        if (u < ntiles) gload(u, u);
+#pragma unroll
+      for (int u = 0; u < A2_SPT; ++u)
+        if (u < ntiles) lstore(u, u);
+#endif
+      __syncthreads();
+      pass(Y{});
+    }
+  }
   if (!active) return;
 
   // ---- row sums to the query's lanes, overflow backstop, normalise, store
 #pragma unroll
   for (int qb = 0; qb < A2_NCH; ++qb) {
-    float ls;
-    if constexpr (F8) {
-      ls = lacc8[qb][0];
-    } else {
-      const float a = __shfl(lacc[qb][0], lane & 15, 64), bsum = __shfl(lacc[qb][1], lane & 15, 64);
-      ls = r < 16 ? a : bsum;
-    }
+    const float ls = rowsum(qb);
     bf16* orow = p.o + ((int64_t)b * p.S + qsrow[qb]) * (p.H * 32) + qh[qb] * 32;
     // some p overflowed the fixed reference (sum >= 2^100, inf or NaN -- tested on the bits:
     // this file builds with -fno-honor-nans): exact recompute

@@ -76,11 +76,12 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* 
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) {
     const int t = 16 * tt + n;
-    const float* xr = X + (int64_t)(t < T ? t : 0) * SE + (int64_t)sr * FR_E + 8 * g;
+    const bool pad = tt == NT - 1 && t >= T;  // only the last tile holds padding (T > 16 (NT - 1))
+    const float* xr = X + (int64_t)(pad ? 0 : t) * SE + (int64_t)sr * FR_E + 8 * g;
 #pragma unroll
     for (int ks = 0; ks < FR_E / 32; ++ks) {
       f32x4 lo = *(const f32x4*)(xr + 32 * ks), hi = *(const f32x4*)(xr + 32 * ks + 4);
-      if (t >= T) lo = hi = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (pad) lo = hi = f32x4{0.f, 0.f, 0.f, 0.f};
       xf[tt][ks] = cat8(lo, hi);
     }
   }
@@ -202,8 +203,9 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* 
         y[f] = mfma16(*(const bf16x8*)(wbuf + (16 * f + n) * FR_ST + 32 * h + 8 * g), of[h][tt], y[f]);
     }
     const int t = 16 * tt + n;
-    const bool valid = rowok && t < T;
-    float* xr = X + (int64_t)(t < T ? t : 0) * SE + (int64_t)sr * FR_E + 4 * g;
+    const bool pad = tt == NT - 1 && t >= T;
+    const bool valid = rowok && !pad;
+    float* xr = X + (int64_t)(pad ? 0 : t) * SE + (int64_t)sr * FR_E + 4 * g;
     float sm = 0.f;
 #pragma unroll
     for (int f = 0; f < FR_E / 16; ++f) {
