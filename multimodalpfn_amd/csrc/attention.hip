@@ -396,6 +396,7 @@ struct Attn2Args {
   int tstart[9];       // task prefix per kv head inside one column
   int64_t kv_bstride;  // elements between the K (V^T) blocks of consecutive columns: H*Npad*32, or
                        // Npad*32 for a head-0-only train-KV cache
+  int q_prescaled;     // Q already carries log2(e)/sqrt(32) (folded into the engine's bf16 Q weights)
 };
 
 __device__ __forceinline__ int a2_koff(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
@@ -500,8 +501,12 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 raw = *(const bf16x8*)(qrow + 16 * ks + 8 * hh);
+      if (p.q_prescaled) {
+        qf[qb][ks] = raw;
+      } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (bf16)((float)raw[e] * c);
+        for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (bf16)((float)raw[e] * c);
+      }
     }
   }
 
@@ -849,7 +854,8 @@ extern "C" int mmpfn_dbg_attn_stamps(void* host) {
 #endif
 
 hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
-                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride) {
+                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride,
+                             bool q_prescaled) {
   if (na + nb <= 0 || T <= 0) return hipSuccess;
   if (nk <= 0 || Npad % A2_KT != 0 || nk > Npad || H > 8 || H <= 0) return hipErrorInvalidValue;
   if (nb > 0 && (kvb < 0 || kvb >= H)) return hipErrorInvalidValue;
@@ -858,6 +864,7 @@ hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void*
   a.S = S, a.H = H, a.Npad = Npad, a.nk = nk;
   a.a0 = a0, a.na = na, a.b0 = b0, a.nb = nb, a.kvb = nb > 0 ? kvb : -1;
   a.kv_bstride = kv_bstride > 0 ? kv_bstride : (int64_t)H * Npad * 32;
+  a.q_prescaled = q_prescaled ? 1 : 0;
   if (kv_bstride > 0 && (na > 0 || kvb != 0)) return hipErrorInvalidValue;  // cache layout holds head 0 only
   int acc = 0;
   for (int g = 0; g < H; ++g) {

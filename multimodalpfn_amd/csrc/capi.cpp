@@ -304,8 +304,15 @@ int finalize(mmpfn_ctx* ctx) {
       wtrain = *wqkv;
       std::copy(wqkv->begin(), wqkv->begin() + (size_t)HD * E, wtest.begin());
     }
-    if ((rc = up2(ctx, L.item_qkv, L.item_qkv_h, wtrain))) return rc;
-    if ((rc = up2(ctx, L.item_qtest, L.item_qtest_h, wtest))) return rc;
+    if ((rc = upload(ctx, L.item_qkv, wtrain, false))) return rc;
+    if ((rc = upload(ctx, L.item_qtest, wtest, false))) return rc;
+    // bf16 copies: the Q rows carry the attention kernel's log2(e)/sqrt(32) (attn_item2 with
+    // q_prescaled: no per-query scaling pass; one bf16 rounding of Q instead of two)
+    const float qsc = 1.4426950408889634f / std::sqrt((float)(E / d.nhead));
+    for (size_t i = 0; i < (size_t)HD * E; ++i) wtrain[i] *= qsc;
+    for (float& w : wtest) w *= qsc;
+    if ((rc = upload(ctx, L.item_qkv_h, wtrain, true))) return rc;
+    if ((rc = upload(ctx, L.item_qtest_h, wtest, true))) return rc;
   }
   int rc;
   {
@@ -639,7 +646,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
     }
     const int64_t cstride = (int64_t)cc->Npad * 32;
     if (bf)
-      HIPCHK(launch_attn_item2(Qi, Kc, Vc, O, S, TM, H, cc->Npad, cc->N, 0, 0, 0, S, 0, st, cstride));
+      HIPCHK(launch_attn_item2(Qi, Kc, Vc, O, S, TM, H, cc->Npad, cc->N, 0, 0, 0, S, 0, st, cstride, true));
     else
       HIPCHK(launch_attn_item(Qi, Kc, Vc, O, S, TM, H, cc->Npad, 0, S, cc->N, 0, prec, st, cstride));
   } else {
@@ -684,7 +691,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
         ctx->kt_flops += 4.0 * TM * (double)(N + Q) * N * E;
         HIPCHK(hipEventRecord(ev[0], st));
       }
-      HIPCHK(launch_attn_item2(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st));
+      HIPCHK(launch_attn_item2(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st, 0, true));
       if (ev) HIPCHK(hipEventRecord(ev[1], st));
     } else {
       HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, 0, N, N, -1, prec, st));

@@ -120,7 +120,8 @@ hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int waves_per_b
 //   kv_bstride > 0: K / V^T hold head 0 only, column blocks kv_bstride elements apart (train-KV
 //   cache; then na = 0 and kvb = 0)
 hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
-                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0);
+                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0,
+                             bool q_prescaled = false);  // Q already scaled by log2(e)/sqrt(32)
 // item attention: queries s in [s0, s0+nq), keys [0, nk); kv_head_fixed >= 0 forces that KV head
 hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
                             int Npad, int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st,
