@@ -49,10 +49,13 @@ def allgather_logits(local: torch.Tensor, assignment: list[list[int]], rank: int
     world = dist.get_world_size(group)
     assert len(assignment) == world and local.shape[0] == len(assignment[rank])
     m_max = max(len(a) for a in assignment)
-    pad = torch.zeros((m_max,) + tail, device=local.device, dtype=local.dtype)
+    # RCCL gathers device tensors in place; a host-only backend (gloo) gathers host copies
+    cdev = local.device if (local.device.type == "cpu" or dist.get_backend(group) != "gloo") else torch.device("cpu")
+    pad = torch.zeros((m_max,) + tail, device=cdev, dtype=local.dtype)
     pad[: local.shape[0]] = local
-    gathered = torch.empty((world * m_max,) + tail, device=local.device, dtype=local.dtype)
+    gathered = torch.empty((world * m_max,) + tail, device=cdev, dtype=local.dtype)
     dist.all_gather_into_tensor(gathered, pad, group=group)
+    gathered = gathered.to(local.device)
     for r, ids in enumerate(assignment):
         if ids:
             out[torch.as_tensor(ids, device=local.device, dtype=torch.long)] = gathered[r * m_max : r * m_max + len(ids)]
