@@ -343,7 +343,7 @@ def timed_steps(step, steps, warmup, world, device):
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], device=device, dtype=torch.float64)
+        tt = torch.tensor([dt], device=device if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     return dt
@@ -467,12 +467,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # rehearsal knobs for a multi-rank run on a box with fewer GPUs than ranks (not for measurement):
+    # MMPFN_BENCH_SHARE_GPUS=1 maps ranks onto the visible GPUs round-robin, MMPFN_BENCH_BACKEND=gloo
+    # replaces RCCL (which refuses two ranks on one GPU)
+    if os.environ.get("MMPFN_BENCH_SHARE_GPUS") == "1":
+        local_rank %= torch.cuda.device_count()
+    backend = os.environ.get("MMPFN_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     import torch.distributed as dist
 
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
 
     from multimodalpfn_amd import _lib
     from multimodalpfn_amd.parallel import lpt_assign
