@@ -28,13 +28,11 @@ namespace {
 
 constexpr int RE = 192;                    // model width
 constexpr int RHC = 32;                    // hidden chunk
-constexpr int W1ST = RE + 16;              // RES Wout staging row stride (bf16): 416 B
 constexpr int SLOT_B = RHC * RE * 2;       // one W1 or W2 chunk image: 12 KB
 constexpr int NSLOT = 3;                   // ring depth per matrix
 constexpr int W2RING = NSLOT * SLOT_B;     // byte offset of the W2 ring
 constexpr int LDS_B = 2 * NSLOT * SLOT_B;  // 72 KB per block: two blocks per CU
 constexpr int MP = SLOT_B / 1024 / 4;      // 1-KB DMA pieces per wave, matrix and chunk (3)
-constexpr int WOUT_E = 2 * SLOT_B / 2;     // RES: Wout staging (bf16 offset) over W1 slot 2 and the W2 ring
 typedef __attribute__((ext_vector_type(2))) float float2_t;
 
 __device__ __forceinline__ void mlp_dma16(uint32_t voff, const void* sbase, unsigned lds_dst) {
@@ -105,8 +103,6 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
   using S2 = std::integral_constant<int, 2>;
-  dma_w1(0, 0);  // under the prologue (W1 slots 0-1 are outside the Wout staging)
-  if (nchunks > 1) dma_w1(1, 1);
 
   // ---- the wave's rows as B fragments in the Y^T lane layout: lane (row 16tt + fr, group fg)
   //      holds features 16f + 4fg + i; K position 32ks + 8fg + j <-> feature of tile f = 2ks + j/4
@@ -121,64 +117,95 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
       af[tt][ks] = b;
     }
   };
-  if constexpr (RES) {
-    // X <- LayerNorm(X + O . Wout^T): Wout [192 out][192 in] staged in two 96-row halves through
-    // the (still unused) weight slots, C^T tiles (lane = row) as in rowgemm_resln
-    bf16x8 ao[TT][RE / 32];
+  auto load_x = [&]() {  // y <- the fp32 residual rows X, in the Y^T accumulator layout
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
       const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
+      const float* xr = X + m * RE + fg * 4;
 #pragma unroll
-      for (int ks = 0; ks < RE / 32; ++ks) ao[tt][ks] = *(const bf16x8*)(O + m * RE + ks * 32 + fg * 8);
+      for (int f = 0; f < RE / 16; ++f) y[f][tt] = *(const f32x4*)(xr + f * 16);
     }
+  };
+  auto wait_vm = [](auto nc) {  // s_waitcnt vmcnt(N): all but this thread's N newest memory ops landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(decltype(nc)::value) : "memory");
+  };
+  using std::integral_constant;
+  // Ring fill order and waits assume three or more chunks (Fh >= 96); fewer drain everything.
+  const bool deep = nchunks >= 3;
+#ifdef MLP_NOPRO  // ablation: skip the out-projection prologue (timing only)
+  if constexpr (false) {
+#else
+  if constexpr (RES) {
+#endif
+    // X <- LayerNorm(X + O . Wout^T): the accumulators start from the residual X, so the out-projection
+    // MFMAs add onto it.  Wout [192 out][192 in] arrives by LDS-DMA in two 96-row halves, swizzled like
+    // the W1 slots, half 0 over the W1 ring and half 1 over the W2 ring, both at kernel start (under
+    // the O / X loads); the W1 ring refills during half 1's MFMAs, the W2 ring during the LayerNorm.
+    {
+      // piece j of this wave: unit q = (wave * 9 + j) * 64 + lane of a half image: row q / 24, unit
+      // (q % 24) ^ ((row >> 1) & 7)
+      uint32_t ow[9];
 #pragma unroll
-    for (int f = 0; f < RE / 16; ++f)
+      for (int j = 0; j < 9; ++j) {
+        const int q = (wave * 9 + j) * 64 + lane, r = q / 24, u = (q % 24) ^ ((r >> 1) & 7);
+        ow[j] = (uint32_t)(r * RE + u * 8) * 2;
+      }
 #pragma unroll
-      for (int tt = 0; tt < TT; ++tt) y[f][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int hf = 0; hf < 2; ++hf) {
+        if (hf == 1) load_x();  // (program order: half 0, O, X, half 1 -- see the waits below)
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      constexpr int PC = 96 * (RE / 8) / 256;  // 16-B pieces per thread (9)
+        for (int j = 0; j < 9; ++j)
+          mlp_dma16(ow[j], Wout + hf * 96 * RE,
+                    __builtin_amdgcn_readfirstlane(lds0 + hf * 3 * SLOT_B + (wave * 9 + j) * 1024));
+        if (hf == 0) {
+          bf16x8 ao[TT][RE / 32];
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {            // three rounds of 3 pieces: bounded staging registers
-        u32x4 st[PC / 3];
+          for (int tt = 0; tt < TT; ++tt) {
+            const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
 #pragma unroll
-        for (int j = 0; j < PC / 3; ++j) {
-          const int pc = tid + 256 * (r * (PC / 3) + j);
-          st[j] = *(const u32x4*)(Wout + (int64_t)(96 * half + pc / 24) * RE + (pc % 24) * 8);
-        }
+            for (int ks = 0; ks < RE / 32; ++ks) ao[tt][ks] = *(const bf16x8*)(O + m * RE + ks * 32 + fg * 8);
+          }
 #pragma unroll
-        for (int j = 0; j < PC / 3; ++j) {
-          const int pc = tid + 256 * (r * (PC / 3) + j);
-          *(u32x4*)(lds + WOUT_E + (pc / 24) * W1ST + (pc % 24) * 8) = st[j];
+          for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+            for (int ks = 0; ks < RE / 32; ++ks) af[tt][ks] = ao[tt][ks];  // O parked in af until the LN
         }
       }
-      __syncthreads();
+    }
+    auto outproj = [&](auto hc) {  // y[6 hf .. 6 hf + 5] += Wout half hf . O^T
+      constexpr int HF = decltype(hc)::value;
 #pragma unroll
       for (int ks = 0; ks < RE / 32; ++ks)
 #pragma unroll
         for (int fl = 0; fl < 6; ++fl) {
-          const bf16x8 w = *(const bf16x8*)(lds + WOUT_E + (fl * 16 + fr) * W1ST + ks * 32 + fg * 8);
+          const bf16x8 w = *(const bf16x8*)(ldsb + HF * 3 * SLOT_B + fl * 16 * 384 + (ks >> 1) * 128 +
+                                            ((ks & 1) ? f1o : f1e));
 #pragma unroll
-          for (int tt = 0; tt < TT; ++tt) y[6 * half + fl][tt] = mfma16(w, ao[tt][ks], y[6 * half + fl][tt]);
+          for (int tt = 0; tt < TT; ++tt) y[6 * HF + fl][tt] = mfma16(w, af[tt][ks], y[6 * HF + fl][tt]);
         }
-      __syncthreads();
-    }
-    // residual + LayerNorm (layer.py:437-455), X' written back (the MLP's residual) and packed
+    };
+    wait_vm(integral_constant<int, 9>{});  // half 0 (and O, X) landed; half 1 may fly
+    __syncthreads();
+    outproj(integral_constant<int, 0>{});
+    __syncthreads();  // every wave is done with half 0: the W1 ring is free
+    dma_w1(0, 0);
+    if (nchunks > 1) dma_w1(1, 1);
+    if (deep) dma_w1(2, 2);
+    if (deep) wait_vm(integral_constant<int, 3 * MP>{});  // half 1 landed; the W1 fills may fly
+    else wait_vm(integral_constant<int, 0>{});
+    __syncthreads();
+    outproj(integral_constant<int, 1>{});
+    __syncthreads();  // the W2 ring is free
+    dma_w2(0, 0);
+    if (nchunks > 1) dma_w2(1, 1);
+    // residual (already in y) + LayerNorm (layer.py:437-455), packed as the MLP's A^T fragments
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
-      const int64_t m = m0 + tt * 16 + fr;
-      const bool valid = m < M;
-      float* xr = X + (valid ? m : (int64_t)M - 1) * RE + fg * 4;
       float sm = 0.f;
 #pragma unroll
-      for (int f = 0; f < RE / 16; ++f) {
-        const f32x4 xv = *(const f32x4*)(xr + f * 16);
+      for (int f = 0; f < RE / 16; ++f)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          y[f][tt][i] += xv[i];
-          sm += y[f][tt][i];
-        }
-      }
+        for (int i = 0; i < 4; ++i) sm += y[f][tt][i];
       const float mean = sum_rows4(sm) * (1.0f / RE);
       float q = 0.f;
 #pragma unroll
@@ -195,24 +222,22 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
         for (int i = 0; i < 4; ++i) y[f][tt][i] = (y[f][tt][i] - mean) * inv;
       to_af(tt);
     }
+    // before H(0): W1(0) landed (newer: W1(1), W1(2), W2(0), W2(1))
+    if (deep) wait_vm(integral_constant<int, 4 * MP>{});
+    else wait_vm(integral_constant<int, 0>{});
   } else {
+    dma_w1(0, 0);
+    if (nchunks > 1) dma_w1(1, 1);
+    load_x();
 #pragma unroll
-    for (int tt = 0; tt < TT; ++tt) {
-      const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
-      const float* xr = X + m * RE + fg * 4;
-#pragma unroll
-      for (int f = 0; f < RE / 16; ++f) y[f][tt] = *(const f32x4*)(xr + f * 16);
-      to_af(tt);
-    }
+    for (int tt = 0; tt < TT; ++tt) to_af(tt);
+    dma_w2(0, 0);
+    if (deep) dma_w1(2, 2);
+    if (nchunks > 1) dma_w2(1, 1);
+    // before H(0): W1(0) landed (newer: W1(1), W2(0), W1(2), W2(1))
+    if (deep) wait_vm(integral_constant<int, 4 * MP>{});
+    else wait_vm(integral_constant<int, 0>{});
   }
-  // (W1 slot 2 and the W2 ring held the RES prologue's Wout staging until its last barrier)
-  dma_w2(0, 0);
-  if (nchunks > 2) dma_w1(2, 2);
-  if (nchunks > 1) dma_w2(1, 1);
-  // before chunk 0: W1(0), W1(1) and W2(0) landed; W1(2) and W2(1) (needed by its end) may fly
-  if (nchunks > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * MP) : "memory");
-  else if (nchunks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MP) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   // H^T [32 hidden][16 TT rows] = W1c . A^T  (W1c in W1 slot SL)
@@ -247,9 +272,11 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
   // accumulate onto it, so the residual is never written out and read back
   f32x4 h[2][TT];
   hmma(S0{}, h);
-  // chunk 0 refills W1 slot 0 (with W1(3)): every wave of the block must have finished reading it
-  // first (a wave can lag a whole chunk behind when another kernel shares its SIMD)
-  if (nchunks > 3) __syncthreads();
+  // before chunk 0: W1(1) and W2(0) landed (only W2(1) may fly); the barrier also keeps chunk 0 from
+  // refilling W1 slot 0 (with W1(3)) while a lagging wave still reads W1(0) above
+  if (deep) wait_vm(integral_constant<int, MP>{});
+  else wait_vm(integral_constant<int, 0>{});
+  __syncthreads();
 
   // one chunk c (PAR = c % 3): reads W1(c+1) from W1 slot (c+1)%3 and W2(c) from W2 slot c%3;
   // refills W1 slot c%3 (W1(c), read in chunk c-1) with W1(c+3) and W2 slot (c+2)%3 (W2(c-1)) with
