@@ -404,9 +404,8 @@ __device__ __forceinline__ int a2_voff(int d, int c) { return d * 128 + 16 * (c 
 
 // exact two-pass softmax for one query per lane, K / V^T straight from global memory
 __device__ __attribute__((noinline)) void a1_exact_rows(const Attn2Args& p, const bf16* Kg, const bf16* Vg,
-                                                         const bf16* qrow, bf16* orow, bool valid) {
-  float q[32], o[32];
-  const float c = kLog2e * 0.17677669529663687f;
+                                                         const bf16* qrow, bf16* orow, bool valid, float c) {
+  float q[32], o[32];  // c: the score scale still to apply to Q (log2(e)/sqrt(32), or 1 when prescaled)
 #pragma unroll
   for (int d = 0; d < 32; ++d) q[d] = (float)qrow[d] * c, o[d] = 0.f;
   float m = -INFINITY;
@@ -825,7 +824,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     if (__any((__float_as_uint(ls) & 0x7fffffffu) >= 0x71800000u)) {
       const bf16* qrow = p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
       // lanes 0-31 own the chain's 32 queries; lanes 32-63 duplicate them and do not store
-      a1_exact_rows(p, Kg, Vg, qrow, orow, qok[qb] && hh == 0);
+      a1_exact_rows(p, Kg, Vg, qrow, orow, qok[qb] && hh == 0, p.q_prescaled ? 1.0f : c);
       continue;
     }
     const float inv = 1.0f / ls;

@@ -1,0 +1,87 @@
+"""Codegen guards for the hot kernels (CPU: hipcc cross-compiles gfx950 to assembly here).
+
+The attention inner loop is issue-bound: its tile body must stay 64 v_exp_f32 +
+32 v_cvt_pk_bf16_f32 + a handful of address ops, with no register shuffles.  An unrelated edit once
+made the compiler re-allocate the loop with ~30 extra v_mov per tile (attention +27 % in time), so the
+tile bodies and the spill counts of the layer kernels are checked on every CPU test run."""
+
+import collections
+import re
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+CSRC = Path(__file__).resolve().parent.parent / "multimodalpfn_amd" / "csrc"
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+
+pytestmark = pytest.mark.skipif(not Path(HIPCC).exists(), reason="hipcc not available")
+
+
+def _asm(src: str, extra=()):
+    out = subprocess.run([HIPCC, *FLAGS, *extra, "-x", "hip", "-S", "--cuda-device-only", str(CSRC / src), "-o", "-"],
+                         capture_output=True, text=True, check=True, timeout=600)
+    return out.stdout
+
+
+def _resources(src: str, extra=()):
+    out = subprocess.run([HIPCC, *FLAGS, *extra, "-x", "hip", "-c", str(CSRC / src), "-o", "/dev/null",
+                          "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, check=True,
+                         timeout=600)
+    res, name = {}, None
+    for ln in out.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", ln)
+        if m:
+            name = m.group(1)
+        m = re.search(r"VGPRs Spill: (\d+)", ln)
+        if m and name:
+            res[name] = int(m.group(1))
+    return res
+
+
+def _function(asm: str, needle: str) -> str:
+    start = re.search(rf"^\S*{needle}\S*:", asm, re.M)
+    assert start, needle
+    end = asm.find(".Lfunc_end", start.end())
+    return asm[start.end():end]
+
+
+def _blocks(body: str) -> list[collections.Counter]:
+    """Instruction counts per basic block (label to label)."""
+    out = []
+    for ln in body.splitlines():
+        if re.match(r"^\.LBB\S+:", ln):
+            out.append(collections.Counter())
+        elif out:
+            m = re.match(r"^\s+([a-z_0-9]+)", ln)
+            if m:
+                out[-1][m.group(1)] += 1
+    return out
+
+
+def test_attention_tile_bodies_have_no_register_shuffles():
+    body = _function(_asm("attention.hip", ["-fno-honor-nans"]), "attn_item2_kernelILb0E")
+    tiles = [c for c in _blocks(body) if c["v_exp_f32_e32"] == 64 and c["v_mfma_f32_32x32x16_bf16"] == 16
+             and c["v_cndmask_b32_e64"] == 0 and c["v_sub_f32_e32"] == 0]
+    assert tiles, "no plain 64-key tile body found"
+    for c in tiles:
+        valu = sum(v for k, v in c.items() if k.startswith("v_"))
+        movs = c["v_mov_b32_e32"] + c["v_mov_b64_e32"]
+        assert movs <= 2 and valu <= 132, (valu, movs)
+
+
+@pytest.mark.parametrize("src,needle,limit", [
+    ("attention.hip", "attn_item2_kernelILb0E", 0),
+    ("mlp_rows.hip", "mlp_rows_kernelILi2ELb1E", 0),
+    ("mlp_rows.hip", "mlp_rows_kernelILi2ELb0E", 0),
+    ("rowgemm.hip", "rowgemm_qkv2_kernel", 0),
+    ("featrow.hip", "feat_rows_kernelILi3E", 48),  # one-time spills outside the head loop
+])
+def test_layer_kernels_spills(src, needle, limit):
+    extra = ["-fno-honor-nans"] if src in ("attention.hip", "featrow.hip") else []
+    res = _resources(src, extra)
+    hits = {k: v for k, v in res.items() if needle in k}
+    assert hits, (needle, list(res))
+    assert max(hits.values()) <= limit, hits
