@@ -250,7 +250,10 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt) h[i][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    constexpr int PU = 2;  // k-steps of W1 fragments in flight ahead of their MFMAs (measured best of 1-3)
+#ifndef MLP_PU
+#define MLP_PU 2
+#endif
+    constexpr int PU = MLP_PU;  // k-steps of W1 fragments in flight ahead of their MFMAs
     bf16x8 wa[PU][2];
 #pragma unroll
     for (int i = 0; i < PU; ++i)
@@ -258,7 +261,9 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
       for (int ht = 0; ht < 2; ++ht) wa[i][ht] = w1frag(ht, i);
 #pragma unroll
     for (int ks = 0; ks < RE / 32; ++ks) {
+#ifndef MLP_NOFENCE1
       __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
@@ -309,14 +314,19 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
     if (MORE) hmma(std::integral_constant<int, (PAR + 1) % 3>{}, h);
     // Y^T [192][32 rows] += W2c(perm) . GELU(H^T)
     {  // W2 fragments 4 tiles ahead of their MFMAs (fenced so the reads stay early; 3-6 measured)
-      constexpr int PF = 4;
+#ifndef MLP_PF
+#define MLP_PF 4
+#endif
+      constexpr int PF = MLP_PF;
       auto w2frag = [&](int o) { return *(const bf16x8*)(ldsb + PAR * SLOT_B + o * 16 * 64 + f2); };
       bf16x8 wb[PF];
 #pragma unroll
       for (int i = 0; i < PF; ++i) wb[i] = w2frag(i);
 #pragma unroll
       for (int o = 0; o < RE / 16; ++o) {
+#ifndef MLP_NOFENCE2
         __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
         for (int tt = 0; tt < TT; ++tt) y[o][tt] = mfma16(wb[o % PF], hb[tt], y[o][tt]);
         if (o + PF < RE / 16) wb[o % PF] = w2frag(o + PF);
