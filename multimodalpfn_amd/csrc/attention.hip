@@ -20,8 +20,6 @@
 //    and combined once at the end.
 //      bf16 : v_mfma_f32_32x32x16_bf16 (4 per 32x64 score tile + 4 for P.V)
 //      f32  : v_mfma_f32_32x32x2_f32 (parity mode; exact fp32 fma chains)
-#include <algorithm>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -399,13 +397,6 @@ struct Attn2Args {
   int64_t kv_bstride;  // elements between the K (V^T) blocks of consecutive columns: H*Npad*32, or
                        // Npad*32 for a head-0-only train-KV cache
   int q_prescaled;     // Q already carries log2(e)/sqrt(32) (folded into the engine's bf16 Q weights)
-  // Dispatch order inside each XCD's task range (launch_attn_item2): its full tasks first, then its
-  // short ones (a head's last chunk of <= 128 queries), so the grid's last round is made of short
-  // blocks.  Long task k: column k / nlong, rank k % nlong -> head by lstart, chunk; short task k:
-  // column k / nshort, head shead[k % nshort], its last chunk.
-  int nlong, nshort;
-  int lstart[9], shead[8];
-  int xl_base[8], xl_n[8], xs_base[8];  // per XCD: first long task, long count, first short task
 };
 
 __device__ __forceinline__ int a2_koff(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
@@ -469,21 +460,14 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
   // ---- task: contiguous task ranges per XCD (blocks of one KV sequence share an L2)
   int b, g, chunk;
   {
-    const int pid = blockIdx.x;
+    const int nbk = p.nblocks, pid = blockIdx.x;
     const int xcd = pid & 7, slot = pid >> 3;
-    if (slot < p.xl_n[xcd]) {  // a full task of this XCD's range
-      const int k = p.xl_base[xcd] + slot;
-      b = k / p.nlong;
-      const int rem = k - b * p.nlong;
-      g = 0;
-      while (g + 1 < p.H && p.lstart[g + 1] <= rem) ++g;
-      chunk = rem - p.lstart[g];
-    } else {  // then its short ones
-      const int k = p.xs_base[xcd] + slot - p.xl_n[xcd];
-      b = k / p.nshort;
-      g = p.shead[k - b * p.nshort];
-      chunk = p.tstart[g + 1] - p.tstart[g] - 1;
-    }
+    const int task = xcd * (nbk >> 3) + min(xcd, nbk & 7) + slot;
+    b = task / p.tasks_per_b;
+    const int rem = task - b * p.tasks_per_b;
+    g = 0;
+    while (g + 1 < p.H && p.tstart[g + 1] <= rem) ++g;
+    chunk = rem - p.tstart[g];
   }
 #ifdef A2_SPRIO  // experiment: static priority for half of the blocks (the later-dispatched CU slots)
   if ((blockIdx.x >> A2_SPRIO) & 1) __builtin_amdgcn_s_setprio(1);
@@ -891,43 +875,6 @@ hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void*
   a.tasks_per_b = acc;
   a.nblocks = acc * T;
   if (a.nblocks == 0) return hipSuccess;
-  // long / short split per head (short: a last chunk of at most half a block of queries)
-  int nlong_g[8], nsh = 0;
-  a.nlong = 0;
-  for (int g = 0; g < H; ++g) {
-    const int cnt = na + (g == a.kvb ? H * nb : 0), nch = a.tstart[g + 1] - a.tstart[g];
-#ifndef A2_ORDER_PLAIN
-    const bool sh = nch > 0 && cnt - (nch - 1) * A2_QPB <= A2_QPB / 2;
-#else
-    const bool sh = false;
-#endif
-    nlong_g[g] = nch - (sh ? 1 : 0);
-    a.lstart[g] = a.nlong;
-    a.nlong += nlong_g[g];
-    if (sh) a.shead[nsh++] = g;
-  }
-  for (int g = H; g < 9; ++g) a.lstart[g] = a.nlong;
-  a.nshort = nsh;
-  // tasks of the original (column, head, chunk) order before global position t, split long / short
-  auto before = [&](int64_t t, bool lng) -> int64_t {
-    const int64_t bb = t / acc;
-    const int r = (int)(t - bb * acc);
-    int64_t n = bb * (lng ? a.nlong : a.nshort);
-    for (int g = 0; g < H; ++g) {
-      const int c0 = a.tstart[g], nch = a.tstart[g + 1] - c0;
-      const int upto = r <= c0 ? 0 : (r >= c0 + nch ? nch : r - c0);  // chunks of g before r
-      n += lng ? std::min(upto, nlong_g[g]) : std::max(0, upto - nlong_g[g]);
-    }
-    return n;
-  };
-  const int nbk = a.nblocks;
-  for (int x = 0; x < 8; ++x) {
-    const int64_t st = (int64_t)x * (nbk >> 3) + std::min(x, nbk & 7);
-    const int64_t en = (int64_t)(x + 1) * (nbk >> 3) + std::min(x + 1, nbk & 7);
-    a.xl_base[x] = (int)before(st, true);
-    a.xl_n[x] = (int)(before(en, true) - a.xl_base[x]);
-    a.xs_base[x] = (int)before(st, false);
-  }
 #ifdef MMPFN_ATTN_FP8PV
   hipLaunchKernelGGL(attn_item2_kernel<true>, dim3(a.nblocks), dim3(256), 0, st, a);
 #else
