@@ -104,7 +104,8 @@ def attn_traffic(T):
     """HBM bytes per attention launch over T token columns, from the committed PMC pass
     (tools/attn_pmc.sh: rocprofv3 FETCH_SIZE and WRITE_SIZE runs at that launch shape)."""
     H, d, S, N = 6, 32, S_ROWS, N_TRAIN
-    for pmc in sorted((ROOT / "profiles" / "r01").glob("attn_item2_pmc*.json")):
+    for pmc in [*sorted((ROOT / "profiles" / "r02").glob("attn_item2_pmc_T*[0-9].json")),
+                *sorted((ROOT / "profiles" / "r01").glob("attn_item2_pmc*.json"))]:  # newest round first
         rec = json.loads(pmc.read_text())
         if rec.get("shape") == {"T": T, "H": H, "d": d, "S": S, "N": N}:
             return rec["hbm_bytes_per_launch"], str(pmc.relative_to(ROOT))
