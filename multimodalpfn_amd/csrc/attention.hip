@@ -570,13 +570,15 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     for (int j = 0; j < 8; ++j) sel[j] = (bf16)(one ? 1.0f : 0.0f);
   }
 
-  f32x16 o[A2_NCH], negm[A2_NCH];
+  f32x16 o[A2_NCH];
+  float mref[A2_NCH];  // the second pass's reference (first tile's row max), one register per chain
   f32x4 lacc[A2_NCH];
   f32x16 lacc8[F8 ? A2_NCH : 1];  // F8 row sums: D rows 0 and 4 (lanes 0-31 and 32-63, register 0)
 #pragma unroll
   for (int qb = 0; qb < A2_NCH; ++qb) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) o[qb][i] = negm[qb][i] = 0.f;
+    for (int i = 0; i < 16; ++i) o[qb][i] = 0.f;
+    mref[qb] = 0.f;
     lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
@@ -590,9 +592,13 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     for (int j = 0; j < 8; ++j) sel8[j] = ones;
   }
 
-  auto tile = [&](int it, auto maskc, auto firstc, auto parc) {
+  // REF: the second pass (scores minus the first tile's row max, subtracted on the VALU: that pass
+  // is rare, and keeping -m as an MFMA accumulator operand would hold 16 registers per chain)
+  auto tile = [&](int it, auto maskc, auto firstc, auto parc, auto refc) {
     constexpr bool MASK = decltype(maskc)::value;
     constexpr bool FIRST = decltype(firstc)::value;
+    constexpr bool REF = decltype(refc)::value;
+    const f32x16 zero16 = {};
     constexpr int PAR = decltype(parc)::value;  // it & 1 (A2_AHEAD == 2: the staging set / LDS slot)
     const int k0 = it * A2_KT;
     const int sub = it % A2_SPT;  // position inside the stage of A2_SPT tiles
@@ -623,7 +629,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 #if defined(A2_PRIO) && A2_PRIO > 1
           __builtin_amdgcn_s_setprio(1);
 #endif
-          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qf[qb][0], negm[qb], 0, 0, 0);
+          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qf[qb][0], zero16, 0, 0, 0);
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][1], qf[qb][1], s[qb][u], 0, 0, 0);
 #if defined(A2_PRIO) && A2_PRIO > 1
           __builtin_amdgcn_s_setprio(0);
@@ -646,13 +652,17 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
           for (int i = 1; i < 16; ++i) m = fmaxf(m, fmaxf(s[qb][0][i], s[qb][1][i]));
           const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
           m = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+          mref[qb] = m;
+        }
+      }
+      if constexpr (REF) {
+#pragma unroll
+        for (int qb = 0; qb < A2_NCH; ++qb)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            negm[qb][i] = -m;
-            s[qb][0][i] -= m;
-            s[qb][1][i] -= m;
+            s[qb][0][i] -= mref[qb];
+            s[qb][1][i] -= mref[qb];
           }
-        }
       }
       if constexpr (F8) {
         const unsigned char* Vs8 = Ks + 4096 + r * 64;
@@ -741,26 +751,26 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     constexpr bool WM = decltype(wmc)::value;
     using F = std::integral_constant<bool, WM>;
     if (ntiles == 1) {
-      if (partial) tile(0, Y{}, F{}, P0{});
-      else tile(0, N{}, F{}, P0{});
+      if (partial) tile(0, Y{}, F{}, P0{}, F{});
+      else tile(0, N{}, F{}, P0{}, F{});
     } else {
-      tile(0, N{}, F{}, P0{});
+      tile(0, N{}, F{}, P0{}, F{});
       A2_STAMP(2);
       const int nfull = p.nk / A2_KT;
 #if A2_AHEAD == 2
       int it = 1;
       for (; it + 1 < nfull; it += 2) {
-        tile(it, N{}, N{}, P1{});
-        tile(it + 1, N{}, N{}, P0{});
+        tile(it, N{}, N{}, P1{}, F{});
+        tile(it + 1, N{}, N{}, P0{}, F{});
       }
-      if (it < nfull) tile(it++, N{}, N{}, P1{});
+      if (it < nfull) tile(it++, N{}, N{}, P1{}, F{});
       if (partial) {
-        if (it & 1) tile(it, Y{}, N{}, P1{});
-        else tile(it, Y{}, N{}, P0{});
+        if (it & 1) tile(it, Y{}, N{}, P1{}, F{});
+        else tile(it, Y{}, N{}, P0{}, F{});
       }
 #else
-      for (int it = 1; it < nfull; ++it) tile(it, N{}, N{}, P0{});
-      if (partial) tile(nfull, Y{}, N{}, P0{});
+      for (int it = 1; it < nfull; ++it) tile(it, N{}, N{}, P0{}, F{});
+      if (partial) tile(nfull, Y{}, N{}, P0{}, F{});
 #endif
     }
   };
@@ -789,7 +799,7 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 #pragma unroll
       for (int qb = 0; qb < A2_NCH; ++qb) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) o[qb][i] = negm[qb][i] = 0.f;
+        for (int i = 0; i < 16; ++i) o[qb][i] = 0.f;
         lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
