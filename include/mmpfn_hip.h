@@ -128,6 +128,8 @@ int mmpfn_status(mmpfn_ctx* ctx);
  * Sample-axis attention for one layout batch:
  *   q  [T][H][S][32], k [T][H][Npad][32], vt [T][H][32][Npad], out [T][S][H*32]
  *   queries s in [s0, s0+nq) attend keys [0, nk); kv_head_fixed >= 0 forces a KV head.
+ *   softmax(q k^T / sqrt(32)): q as projected (the engine's own bf16 forward passes q pre-multiplied
+ *   by log2(e)/sqrt(32) internally; these taps do not).
  * Element type: fp32 (MMPFN_PREC_F32) or bf16 (MMPFN_PREC_BF16). */
 int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S, int T,
                          int H, int Npad, int s0, int nq, int nk, int kv_head_fixed, int precision);
