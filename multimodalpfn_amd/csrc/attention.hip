@@ -779,8 +779,11 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     if constexpr (F8) {
       return lacc8[qb][0];
     } else {
-      const float a = __shfl(lacc[qb][0], lane & 15, 64), bsum = __shfl(lacc[qb][1], lane & 15, 64);
-      return r < 16 ? a : bsum;
+      // D rows 0 / 1 (queries 0-15 / 16-31) sit in lanes 0-15, registers 0 / 1
+      const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(lacc[qb][0]), __float_as_uint(lacc[qb][1]),
+                                                      false, false);  // lanes 16-31 <- register 1 of 0-15
+      const auto s2 = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);  // lanes 32-63 <- 0-31
+      return __uint_as_float(s2[0]);
     }
   };
   pass(N{});
@@ -838,14 +841,23 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
       continue;
     }
     const float inv = 1.0f / ls;
-    if (qok[qb]) {
+    // lane (r, hh) holds d = 8 gq + 4 hh + 0..3; permlane32_swap(a, b) gives lanes 32-63 the b of lanes
+    // 0-31 (first result) and lanes 0-31 the a of lanes 32-63 (second): 16-B stores of d 8g .. 8g+7
+    // (lanes 0-31) and 8g+8 .. 8g+15 (lanes 32-63), g = 0, 2
+    u32x2 w[4];
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        bf16x4 w;
+    for (int gq = 0; gq < 4; ++gq) {
+      bf16x4 v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = (bf16)(o[qb][4 * gq + e] * inv);
-        *(bf16x4*)(orow + 8 * gq + 4 * hh) = w;
-      }
+      for (int e = 0; e < 4; ++e) v[e] = (bf16)(o[qb][4 * gq + e] * inv);
+      w[gq] = __builtin_bit_cast(u32x2, v);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; g += 2) {
+      const auto sx = __builtin_amdgcn_permlane32_swap(w[g].x, w[g + 1].x, false, false);
+      const auto sy = __builtin_amdgcn_permlane32_swap(w[g].y, w[g + 1].y, false, false);
+      const u32x4 st = hh == 0 ? u32x4{w[g].x, w[g].y, sx[1], sy[1]} : u32x4{sx[0], sy[0], w[g + 1].x, w[g + 1].y};
+      if (qok[qb]) *(u32x4*)(orow + 8 * g + 8 * hh) = st;
     }
   }
 #ifdef A2_STAMPS
