@@ -2,7 +2,7 @@
 # rocprofv3 kernel trace + stats of the headline step at one lane (kernels one after another): the
 # per-kernel durations the bench line's `roofline` (one-lane pass) is measured on.
 set -o pipefail
-R=$PWD; TAG=${1:-run}; O=$R/gpurun_out/${TAG}_lanes1; mkdir -p $O  # own dir: evidence.sh uses $TAG; export TMPDIR=/tmp
+R=$PWD; TAG=${1:-run}; O=$R/gpurun_out/${TAG}_lanes1; mkdir -p $O; export TMPDIR=/tmp  # own dir: evidence.sh writes $TAG
 cd /tmp || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/rprof -o run --output-format csv -- \
   python3 $R/bench.py --lanes 1 --steps 10 --warmup 3 --no-cpu-baseline --no-modality --no-config-d --no-f32 \
