@@ -41,6 +41,15 @@ __device__ __forceinline__ void mlp_dma16(uint32_t voff, const void* sbase, unsi
                : "memory");
 }
 
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {  // f(integral_constant<int, 0>) .. f(<N - 1>)
+  static_for_(f, std::make_integer_sequence<int, N>{});
+}
+
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -240,8 +249,23 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
   }
   __syncthreads();
 
-  // H^T [32 hidden][16 TT rows] = W1c . A^T  (W1c in W1 slot SL)
-  auto hmma = [&](auto slc, f32x4 (&h)[2][TT]) {
+  // GELU of one adjacent pair q (0 .. 4 TT - 1: tile tt, half ht, elements 2 (q & 1) + 0, 1) of a chunk's
+  // H^T accumulators, packed into its bf16 B fragment for the down-projection
+  auto gelu_pair = [&](auto qc, const f32x4 (&hs)[2][TT], bf16x8 (&hb)[TT]) {
+    constexpr int q = decltype(qc)::value, tt = q >> 2, ht = (q >> 1) & 1, i = 2 * (q & 1);
+#ifndef MLP_NOGELU
+    const bf16x2 pr =
+        __builtin_convertvector((float2_t){gelu_tanh_fast(hs[ht][tt][i]), gelu_tanh_fast(hs[ht][tt][i + 1])}, bf16x2);
+#else  // ablation: identity activation
+    const bf16x2 pr = __builtin_convertvector((float2_t){hs[ht][tt][i], hs[ht][tt][i + 1]}, bf16x2);
+#endif
+    hb[tt][4 * ht + i] = pr[0];
+    hb[tt][4 * ht + i + 1] = pr[1];
+  };
+  // H^T [32 hidden][16 TT rows] = W1c . A^T  (W1c in W1 slot SL); with G, the previous chunk's GELU
+  // (hs -> hb) rides in the k-steps' MFMA shadows (pairs 0..4TT-1 spread over the RE/32 k-steps)
+  auto hmma = [&](auto slc, f32x4 (&h)[2][TT], auto gc, const f32x4 (&hs)[2][TT], bf16x8 (&hb)[TT]) {
+    constexpr bool G = decltype(gc)::value;
     constexpr int SL = decltype(slc)::value;
     auto w1frag = [&](int ht, int ks) {
       return *(const bf16x8*)(ldsb + SL * SLOT_B + ht * 16 * 384 + (ks >> 1) * 128 + ((ks & 1) ? f1o : f1e));
@@ -271,12 +295,22 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
       if (ks + PU < RE / 32)
 #pragma unroll
         for (int ht = 0; ht < 2; ++ht) wa[ks % PU][ht] = w1frag(ht, ks + PU);
+      if constexpr (G) {  // pairs [ks * NPQ / NKS, (ks + 1) * NPQ / NKS)
+        constexpr int NPQ = 4 * TT, NKS = RE / 32;
+        static_for<NPQ>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          if (q * NKS / NPQ == ks) gelu_pair(qc, hs, hb);
+        });
+      }
     }
   };
   // y holds the residual (X, or X' after the fused prologue) in fp32: the down-projection MFMAs
   // accumulate onto it, so the residual is never written out and read back
   f32x4 h[2][TT];
-  hmma(S0{}, h);
+  {
+    bf16x8 unused[TT];
+    hmma(S0{}, h, std::false_type{}, h, unused);
+  }
   // before chunk 0: W1(1) and W2(0) landed (only W2(1) may fly); the barrier also keeps chunk 0 from
   // refilling W1 slot 0 (with W1(3)) while a lagging wave still reads W1(0) above
   if (deep) wait_vm(integral_constant<int, MP>{});
@@ -294,24 +328,17 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
     if (d1) dma_w1(c + 3, PAR);
     if (d2) dma_w2(c + 2, (PAR + 2) % 3);
 #endif
-    bf16x8 hb[TT];  // GELU of chunk c (VALU) beside the up-projection MFMAs of chunk c+1
-#pragma unroll
-    for (int tt = 0; tt < TT; ++tt) {
+    bf16x8 hb[TT];  // GELU of chunk c (VALU) inside the up-projection MFMAs of chunk c+1
+    if (MORE) {
+      f32x4 hn[2][TT];
+      hmma(std::integral_constant<int, (PAR + 1) % 3>{}, hn, std::true_type{}, h, hb);
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-        for (int i = 0; i < 4; i += 2) {  // adjacent pairs: one v_cvt_pk_bf16_f32 each
-#ifndef MLP_NOGELU
-          const bf16x2 pr = __builtin_convertvector(
-              (float2_t){gelu_tanh_fast(h[ht][tt][i]), gelu_tanh_fast(h[ht][tt][i + 1])}, bf16x2);
-#else  // ablation: identity activation
-          const bf16x2 pr = __builtin_convertvector((float2_t){h[ht][tt][i], h[ht][tt][i + 1]}, bf16x2);
-#endif
-          hb[tt][4 * ht + i] = pr[0];
-          hb[tt][4 * ht + i + 1] = pr[1];
-        }
+        for (int tt = 0; tt < TT; ++tt) h[ht][tt] = hn[ht][tt];
+    } else {
+      static_for<4 * TT>([&](auto qc) { gelu_pair(qc, h, hb); });
     }
-    if (MORE) hmma(std::integral_constant<int, (PAR + 1) % 3>{}, h);
     // Y^T [192][32 rows] += W2c(perm) . GELU(H^T)
     {  // W2 fragments 4 tiles ahead of their MFMAs (fenced so the reads stay early; 3-6 measured)
 #ifndef MLP_PF
