@@ -57,15 +57,19 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // TT = 16-row tiles per wave: 2 (32 rows, two waves per SIMD, accumulators in VGPRs) or 4 (64 rows,
 // one wave per SIMD with the 192 x 64 Y^T accumulator in AGPRs -- half the LDS weight reads per row,
 // but measured 15% slower: one wave cannot hide the LDS / GELU latency the second wave covers)
-template <int TT, bool RES>
-__global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* __restrict__ X,
+// NW = waves per block: 4 (two blocks per CU, each DMA-filling its own rings) or 8 (one block per CU:
+// each weight byte crosses into LDS once per CU; waves 0-3 fill the W1 ring, 4-7 the W2 ring)
+template <int TT, bool RES, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_rows_kernel(float* __restrict__ X,
                                                                        const bf16* __restrict__ W1,
                                                                        const bf16* __restrict__ W2p, int M, int Fh,
                                                                        float eps, const bf16* __restrict__ O,
                                                                        const bf16* __restrict__ Wout) {
-  constexpr int RROWS = 4 * 16 * TT;  // rows per block
+  constexpr int RROWS = NW * 16 * TT;  // rows per block
   __shared__ __attribute__((aligned(1024))) bf16 lds[LDS_B / 2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wg = wave & 3;                           // the wave's share of a ring fill
+  const bool gw1 = NW == 4 || wave < 4, gw2 = NW == 4 || wave >= 4;  // fills W1 / W2 pieces
   const int fr = lane & 15, fg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * RROWS + wave * 16 * TT;
   const int nchunks = Fh / RHC;
@@ -85,24 +89,26 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
   uint32_t o1[MP], o2[MP];
 #pragma unroll
   for (int j = 0; j < MP; ++j) {
-    const int q = (wave * MP + j) * 64 + lane;  // unit index inside a slot image
+    const int q = (wg * MP + j) * 64 + lane;  // unit index inside a slot image
     const int r1 = q / 24, u1 = (q % 24) ^ ((r1 >> 1) & 7);
     o1[j] = (uint32_t)(r1 * RE + u1 * 8) * 2;
     const int r2 = q >> 2, u2 = (q & 3) ^ ((r2 >> 2) & 2);
     o2[j] = (uint32_t)(r2 * Fh + u2 * 8) * 2;
   }
   auto dma_w1 = [&](int c, int slot) {  // W1 rows c*32 .. +31
+    if (!gw1) return;
     const bf16* base = W1 + (int64_t)c * RHC * RE;
 #pragma unroll
     for (int j = 0; j < MP; ++j)
-      mlp_dma16(o1[j], base, __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT_B + (wave * MP + j) * 1024));
+      mlp_dma16(o1[j], base, __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT_B + (wg * MP + j) * 1024));
   };
   auto dma_w2 = [&](int c, int slot) {  // W2 columns c*32 .. +31 (permuted), all 192 rows
+    if (!gw2) return;
     const bf16* base = W2p + c * RHC;
 #pragma unroll
     for (int j = 0; j < MP; ++j)
       mlp_dma16(o2[j], base,
-                __builtin_amdgcn_readfirstlane(lds0 + W2RING + slot * SLOT_B + (wave * MP + j) * 1024));
+                __builtin_amdgcn_readfirstlane(lds0 + W2RING + slot * SLOT_B + (wg * MP + j) * 1024));
   };
   // fragment read offsets (bytes inside a slot): W1 row 16 ht + fr, unit 4 ks + fg; W2 row 16 o + fr, unit fg
   const int s1 = (fr >> 1) & 7;
@@ -156,16 +162,17 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
       uint32_t ow[9];
 #pragma unroll
       for (int j = 0; j < 9; ++j) {
-        const int q = (wave * 9 + j) * 64 + lane, r = q / 24, u = (q % 24) ^ ((r >> 1) & 7);
+        const int q = (wg * 9 + j) * 64 + lane, r = q / 24, u = (q % 24) ^ ((r >> 1) & 7);
         ow[j] = (uint32_t)(r * RE + u * 8) * 2;
       }
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         if (hf == 1) load_x();  // (program order: half 0, O, X, half 1 -- see the waits below)
+        if (NW == 4 || (wave >> 2) == hf)  // NW 8: waves 0-3 half 0, 4-7 half 1
 #pragma unroll
-        for (int j = 0; j < 9; ++j)
-          mlp_dma16(ow[j], Wout + hf * 96 * RE,
-                    __builtin_amdgcn_readfirstlane(lds0 + hf * 3 * SLOT_B + (wave * 9 + j) * 1024));
+          for (int j = 0; j < 9; ++j)
+            mlp_dma16(ow[j], Wout + hf * 96 * RE,
+                      __builtin_amdgcn_readfirstlane(lds0 + hf * 3 * SLOT_B + (wg * 9 + j) * 1024));
         if (hf == 0) {
           bf16x8 ao[TT][RE / 32];
 #pragma unroll
@@ -200,7 +207,8 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
     dma_w1(0, 0);
     if (nchunks > 1) dma_w1(1, 1);
     if (deep) dma_w1(2, 2);
-    if (deep) wait_vm(integral_constant<int, 3 * MP>{});  // half 1 landed; the W1 fills may fly
+    // half 1 landed, the W1 fills may fly (NW 8: waves 0-3 hold no half-1 pieces, 4-7 no W1 fills)
+    if (deep && gw1) wait_vm(integral_constant<int, 3 * MP>{});
     else wait_vm(integral_constant<int, 0>{});
     __syncthreads();
     outproj(integral_constant<int, 1>{});
@@ -231,8 +239,8 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
         for (int i = 0; i < 4; ++i) y[f][tt][i] = (y[f][tt][i] - mean) * inv;
       to_af(tt);
     }
-    // before H(0): W1(0) landed (newer: W1(1), W1(2), W2(0), W2(1))
-    if (deep) wait_vm(integral_constant<int, 4 * MP>{});
+    // before H(0): W1(0) landed (newer: W1(1), W1(2), W2(0), W2(1); NW 8: each group its own two)
+    if (deep) wait_vm(integral_constant<int, (NW == 8 ? 2 : 4) * MP>{});
     else wait_vm(integral_constant<int, 0>{});
   } else {
     dma_w1(0, 0);
@@ -243,8 +251,8 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
     dma_w2(0, 0);
     if (deep) dma_w1(2, 2);
     if (nchunks > 1) dma_w2(1, 1);
-    // before H(0): W1(0) landed (newer: W1(1), W2(0), W1(2), W2(1))
-    if (deep) wait_vm(integral_constant<int, 4 * MP>{});
+    // before H(0): W1(0) landed (newer: W1(1), W2(0), W1(2), W2(1); NW 8: W1(1), X, W1(2))
+    if (deep) wait_vm(integral_constant<int, (NW == 8 ? 2 : 4) * MP>{});
     else wait_vm(integral_constant<int, 0>{});
   }
   __syncthreads();
@@ -324,7 +332,7 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
     const bool MORE = c + 1 < nchunks;  // a chunk c+1 exists (wave-uniform)
     constexpr int PAR = decltype(parc)::value;
     [[maybe_unused]] const bool d1 = c + 3 < nchunks, d2 = c + 2 < nchunks;
-#ifndef MLP_NOSTAGE
+#if !defined(MLP_NOSTAGE) && !defined(MLP_NODMA)
     if (d1) dma_w1(c + 3, PAR);
     if (d2) dma_w2(c + 2, (PAR + 2) % 3);
 #endif
@@ -360,11 +368,16 @@ __global__ __launch_bounds__(256, TT == 2 ? 2 : 1) void mlp_rows_kernel(float* _
       }
     }
     if (MORE) {
-#ifndef MLP_NOSTAGE
+#if !defined(MLP_NOSTAGE) && !defined(MLP_NOWAIT)  // (ablations: timing only)
       // this thread's pieces of W1(c+2) and W2(c+1) landed; this chunk's own fills may still fly
-      if (d1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * MP) : "memory");
-      else if (d2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MP) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (NW == 8) {  // one matrix per wave
+        if (gw1 ? d1 : d2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MP) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        if (d1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * MP) : "memory");
+        else if (d2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MP) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
 #endif
 #ifndef MLP_NOSYNC
       __syncthreads();
@@ -427,13 +440,16 @@ hipError_t launch_mlp_rows(float* X, const void* W1perm, const void* W2perm, int
 #ifndef MLP_TT
 #define MLP_TT 2  // 4 measured slower: 202 vs 175 us per two-member launch
 #endif
-  constexpr int RROWS = 64 * MLP_TT;
-  const dim3 grid((unsigned)((M + RROWS - 1) / RROWS)), block(256);
+#ifndef MLP_NW
+#define MLP_NW 4  // 8 measured slower: 175.3 vs 162.8 us (one block per CU: its waves hit the barriers in step)
+#endif
+  constexpr int RROWS = 16 * MLP_NW * MLP_TT;
+  const dim3 grid((unsigned)((M + RROWS - 1) / RROWS)), block(64 * MLP_NW);
   if (O)
-    hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, true>), grid, block, 0, st, X, (const bf16*)W1perm,
+    hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, true, MLP_NW>), grid, block, 0, st, X, (const bf16*)W1perm,
                        (const bf16*)W2perm, (int)M, Fh, eps, (const bf16*)O, (const bf16*)Wout);
   else
-    hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, false>), grid, block, 0, st, X, (const bf16*)W1perm,
+    hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, false, MLP_NW>), grid, block, 0, st, X, (const bf16*)W1perm,
                        (const bf16*)W2perm, (int)M, Fh, eps, nullptr, nullptr);
   return hipGetLastError();
 }
