@@ -465,9 +465,14 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
     const int task = xcd * (nbk >> 3) + min(xcd, nbk & 7) + slot;
     b = task / p.tasks_per_b;
     const int rem = task - b * p.tasks_per_b;
+    // g = the last head whose task prefix is <= rem (tstart is non-decreasing); constant indices, so
+    // the prefixes come with the other kernel arguments instead of a chain of dependent loads
     g = 0;
-    while (g + 1 < p.H && p.tstart[g + 1] <= rem) ++g;
-    chunk = rem - p.tstart[g];
+    int base = p.tstart[0];
+#pragma unroll
+    for (int h = 1; h < 9; ++h)
+      if (h < p.H && p.tstart[h] <= rem) g = h, base = p.tstart[h];
+    chunk = rem - base;
   }
 #ifdef A2_SPRIO  // experiment: static priority for half of the blocks (the later-dispatched CU slots)
   if ((blockIdx.x >> A2_SPRIO) & 1) __builtin_amdgcn_s_setprio(1);
