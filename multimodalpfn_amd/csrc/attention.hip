@@ -891,6 +891,9 @@ hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void*
   a.a0 = a0, a.na = na, a.b0 = b0, a.nb = nb, a.kvb = nb > 0 ? kvb : -1;
   a.kv_bstride = kv_bstride > 0 ? kv_bstride : (int64_t)H * Npad * 32;
   a.q_prescaled = q_prescaled ? 1 : 0;
+#ifdef A2_STAMPS  // diagnostics: time the engine's prescaled-Q prologue through the raw tap
+  if (getenv("A2_STAMPS_PRESCALED")) a.q_prescaled = 1;
+#endif
   if (kv_bstride > 0 && (na > 0 || kvb != 0)) return hipErrorInvalidValue;  // cache layout holds head 0 only
   int acc = 0;
   for (int g = 0; g < H; ++g) {
