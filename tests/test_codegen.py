@@ -85,3 +85,20 @@ def test_layer_kernels_spills(src, needle, limit):
     hits = {k: v for k, v in res.items() if needle in k}
     assert hits, (needle, list(res))
     assert max(hits.values()) <= limit, hits
+
+
+def test_mlp_gelu_rides_in_the_up_projection():
+    """The previous chunk's GELU once sank past the `if (MORE) hmma` branch into the down-projection's
+    block, whose MFMAs consume it.  Now every in-loop up-projection block carries the
+    GELU; only the pre-loop up-projection of chunk 0 has none to carry."""
+    body = _function(_asm("mlp_rows.hip"), "mlp_rows_kernelILi2ELb1E")
+    up = [c for c in _blocks(body) if c["v_mfma_f32_16x16x32_bf16"] == 24]
+    bare = [c for c in up if c["v_exp_f32_e32"] == 0]
+    carrying = [c for c in up if c["v_exp_f32_e32"] >= 12]
+    assert len(bare) <= 1 and carrying, ([(c["v_mfma_f32_16x16x32_bf16"], c["v_exp_f32_e32"]) for c in up])
+
+
+def test_mlp_eight_wave_option_does_not_spill():
+    res = _resources("mlp_rows.hip", ["-DMLP_NW=8"])
+    hits = {k: v for k, v in res.items() if "mlp_rows_kernelILi2ELb1ELi8E" in k}
+    assert hits and max(hits.values()) == 0, hits
