@@ -89,13 +89,14 @@ def test_layer_kernels_spills(src, needle, limit):
 
 def test_mlp_gelu_rides_in_the_up_projection():
     """The previous chunk's GELU once sank past the `if (MORE) hmma` branch into the down-projection's
-    block, whose MFMAs consume it.  Now every in-loop up-projection block carries the
-    GELU; only the pre-loop up-projection of chunk 0 has none to carry."""
+    block, whose MFMAs consume it.  Now each chunk is one block (up-projection of the next
+    chunk + this chunk's GELU + down-projection, 48 MFMAs, 16 exps); only the pre-loop up-projection of
+    chunk 0 (24 MFMAs) has no GELU to carry."""
     body = _function(_asm("mlp_rows.hip"), "mlp_rows_kernelILi2ELb1E")
-    up = [c for c in _blocks(body) if c["v_mfma_f32_16x16x32_bf16"] == 24]
-    bare = [c for c in up if c["v_exp_f32_e32"] == 0]
-    carrying = [c for c in up if c["v_exp_f32_e32"] >= 12]
-    assert len(bare) <= 1 and carrying, ([(c["v_mfma_f32_16x16x32_bf16"], c["v_exp_f32_e32"]) for c in up])
+    mm = [c for c in _blocks(body) if 24 <= c["v_mfma_f32_16x16x32_bf16"] < 72]
+    bare = [c for c in mm if c["v_exp_f32_e32"] == 0]
+    chunks = [c for c in mm if c["v_mfma_f32_16x16x32_bf16"] == 48 and c["v_exp_f32_e32"] == 16]
+    assert len(bare) <= 1 and len(chunks) >= 3, ([(c["v_mfma_f32_16x16x32_bf16"], c["v_exp_f32_e32"]) for c in mm])
 
 
 def test_mlp_eight_wave_option_does_not_spill():
