@@ -126,13 +126,24 @@ MODALITY_SIGNATURES = [
 _LIB = None
 
 
+def diagnostics_enabled() -> bool:
+    """``MMPFN_DIAGNOSTICS=1``: the only way a variant library (an A/B or stamps build) may be loaded."""
+    return os.environ.get("MMPFN_DIAGNOSTICS") == "1"
+
+
 def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
-    """Load ``libmmpfn_hip.so`` (loud failure, no fallback)."""
+    """Load ``libmmpfn_hip.so`` (loud failure, no fallback).
+
+    Variant builds (``tools/build_variant*.sh``, ``make dbg``) export ``mmpfn_variant_flags`` and
+    are refused unless ``MMPFN_DIAGNOSTICS=1``; so is any library named by ``MMPFN_LIB``.  The product
+    path therefore only ever runs the in-tree production build."""
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    # MMPFN_LIB: diagnostics only (e.g. the stamps build of `make dbg`)
-    p = Path(path) if path is not None else Path(os.environ.get("MMPFN_LIB") or str(LIB_PATH))
+    env = os.environ.get("MMPFN_LIB")
+    if path is None and env and not diagnostics_enabled():
+        raise RuntimeError("MMPFN_LIB names a diagnostics library; set MMPFN_DIAGNOSTICS=1 to load it")
+    p = Path(path) if path is not None else Path(env or str(LIB_PATH))
     if not p.exists():
         raise RuntimeError(
             f"MMPFN HIP engine library not found at {p}; build it with "
@@ -142,6 +153,9 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     import torch  # noqa: F401
 
     lib = ctypes.CDLL(str(p))
+    if hasattr(lib, "mmpfn_variant_flags") and not diagnostics_enabled():
+        flags = ctypes.c_char_p.in_dll(lib, "mmpfn_variant_flags").value
+        raise RuntimeError(f"{p} is a variant build ({flags!r}); set MMPFN_DIAGNOSTICS=1 to load it")
     for name, res, args in SIGNATURES + MODALITY_SIGNATURES:
         fn = getattr(lib, name)
         fn.restype = res

@@ -289,12 +289,8 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
         }
       }
     }
-#ifndef A2_NOSTAGE
     if (it + 1 < ntiles) lstore((it + 1) & 1);
-#endif
-#ifndef A2_NOSYNC
     __syncthreads();
-#endif
   };
 
   gload(0, std::bool_constant<true>{});  // masking is a no-op unless the tile is partial
@@ -474,9 +470,6 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
       if (h < p.H && p.tstart[h] <= rem) g = h, base = p.tstart[h];
     chunk = rem - base;
   }
-#ifdef A2_SPRIO  // experiment: static priority for half of the blocks (the later-dispatched CU slots)
-  if ((blockIdx.x >> A2_SPRIO) & 1) __builtin_amdgcn_s_setprio(1);
-#endif
   const int cnt = p.na + (g == p.kvb ? p.H * p.nb : 0);
   const int jw = chunk * A2_QPB + wave * A2_QPW;  // first query of this wave
   const bool active = jw < cnt;               // wave-uniform
@@ -631,14 +624,8 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
       for (int qb = 0; qb < A2_NCH; ++qb)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-#if defined(A2_PRIO) && A2_PRIO > 1
-          __builtin_amdgcn_s_setprio(1);
-#endif
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qf[qb][0], zero16, 0, 0, 0);
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][1], qf[qb][1], s[qb][u], 0, 0, 0);
-#if defined(A2_PRIO) && A2_PRIO > 1
-          __builtin_amdgcn_s_setprio(0);
-#endif
         }
       if constexpr (MASK) {
 #pragma unroll
@@ -700,21 +687,9 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
           for (int sp = 0; sp < 2; ++sp) {
             bf16x8 pb;
 #pragma unroll
-#ifndef A2_NOEXP
             for (int j = 0; j < 8; ++j) pb[j] = (bf16)__builtin_amdgcn_exp2f(s[qb][u][8 * sp + j]);
-#else
-            for (int j = 0; j < 8; ++j) pb[j] = (bf16)s[qb][u][8 * sp + j];
-#endif
-#ifdef A2_PRIO
-            __builtin_amdgcn_s_setprio(1);
-#endif
             o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[u][sp], pb, o[qb], 0, 0, 0);
-#ifndef A2_NOSEL
             lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[qb], 0, 0, 0);
-#endif
-#ifdef A2_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
           }
     }
 #if A2_AHEAD == 2

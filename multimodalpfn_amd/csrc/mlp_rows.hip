@@ -147,11 +147,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
   using std::integral_constant;
   // Ring fill order and waits assume three or more chunks (Fh >= 96); fewer drain everything.
   const bool deep = nchunks >= 3;
-#ifdef MLP_NOPRO  // ablation: skip the out-projection prologue (timing only)
-  if constexpr (false) {
-#else
   if constexpr (RES) {
-#endif
     // X <- LayerNorm(X + O . Wout^T): the accumulators start from the residual X, so the out-projection
     // MFMAs add onto it.  Wout [192 out][192 in] arrives by LDS-DMA in two 96-row halves, swizzled like
     // the W1 slots, half 0 over the W1 ring and half 1 over the W2 ring, both at kernel start (under
@@ -261,12 +257,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
   // H^T accumulators, packed into its bf16 B fragment for the down-projection
   auto gelu_pair = [&](auto qc, const f32x4 (&hs)[2][TT], bf16x8 (&hb)[TT]) {
     constexpr int q = decltype(qc)::value, tt = q >> 2, ht = (q >> 1) & 1, i = 2 * (q & 1);
-#ifndef MLP_NOGELU
     const bf16x2 pr =
         __builtin_convertvector((float2_t){gelu_tanh_fast(hs[ht][tt][i]), gelu_tanh_fast(hs[ht][tt][i + 1])}, bf16x2);
-#else  // ablation: identity activation
-    const bf16x2 pr = __builtin_convertvector((float2_t){hs[ht][tt][i], hs[ht][tt][i + 1]}, bf16x2);
-#endif
     hb[tt][4 * ht + i] = pr[0];
     hb[tt][4 * ht + i + 1] = pr[1];
   };
@@ -293,9 +285,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
       for (int ht = 0; ht < 2; ++ht) wa[i][ht] = w1frag(ht, i);
 #pragma unroll
     for (int ks = 0; ks < RE / 32; ++ks) {
-#ifndef MLP_NOFENCE1
       __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
@@ -332,10 +322,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     const bool MORE = c + 1 < nchunks;  // a chunk c+1 exists (wave-uniform)
     constexpr int PAR = decltype(parc)::value;
     [[maybe_unused]] const bool d1 = c + 3 < nchunks, d2 = c + 2 < nchunks;
-#if !defined(MLP_NOSTAGE) && !defined(MLP_NODMA)
     if (d1) dma_w1(c + 3, PAR);
     if (d2) dma_w2(c + 2, (PAR + 2) % 3);
-#endif
     // GELU of chunk c (VALU) inside the up-projection MFMAs of chunk c+1.  No branch on MORE: the last
     // chunk's up-projection reads a slot holding an older chunk (landed, unused result), which costs 1/24
     // of the up-projections and measured 0.7 % faster than the branch (159.9 -> 158.8 us)
@@ -360,16 +348,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
       for (int i = 0; i < PF; ++i) wb[i] = w2frag(i);
 #pragma unroll
       for (int o = 0; o < RE / 16; ++o) {
-#ifndef MLP_NOFENCE2
         __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
         for (int tt = 0; tt < TT; ++tt) y[o][tt] = mfma16(wb[o % PF], hb[tt], y[o][tt]);
         if (o + PF < RE / 16) wb[o % PF] = w2frag(o + PF);
       }
     }
     if (MORE) {
-#if !defined(MLP_NOSTAGE) && !defined(MLP_NOWAIT)  // (ablations: timing only)
       // this thread's pieces of W1(c+2) and W2(c+1) landed; this chunk's own fills may still fly
       if constexpr (NW == 8) {  // one matrix per wave
         if (gw1 ? d1 : d2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MP) : "memory");
@@ -379,10 +364,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
         else if (d2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MP) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-#endif
-#ifndef MLP_NOSYNC
       __syncthreads();
-#endif
     }
   };
   // unrolled by three so that every ring slot is a compile-time offset (no peeled copies: the last
@@ -422,11 +404,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
         f32x4 ov;
 #pragma unroll
         for (int i = 0; i < 4; ++i) ov[i] = (y[o][tt][i] - mean) * inv;
-#ifndef MLP_NOSTORE
         *(f32x4*)(xr + o * 16) = ov;
-#else
-        if (ov[0] == 1234.5f && ov[3] == 4321.f) xr[o] = ov[1];
-#endif
       }
     }
   }

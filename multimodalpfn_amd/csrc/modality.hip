@@ -111,11 +111,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tile_kernel(const bf16* __restric
   // DMA: slice s >= TNST is issued in phase 2(s - TNST) + 2 (its stage was last read, by group 1, in
   // phase 2(s - TNST) + 1); each wave waits for its own pieces of slice j before the barrier that
   // ends phase 2j - 1, so slice j is complete and visible when group 0 reads it in phase 2j.
-#ifdef GT_NOLOOP  // diagnostics variant: epilogue only (timing only)
-  const int nk = 0;
-#else
   const int nk = K / TK;
-#endif
 #pragma unroll
   for (int i = 0; i < TNST; ++i)
     if (i < nk) dma(i);
@@ -144,25 +140,16 @@ __global__ __launch_bounds__(512, 1) void gemm_tile_kernel(const bf16* __restric
     }
   };
   auto compute = [&]() {
-#ifdef GT_NOMFMA  // diagnostics variant: no matrix work (timing only)
-    return;
-#endif
-#ifndef GT_NOPRIO
     __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
     for (int a = 0; a < TMT; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bw[b], acc[a][b], 0, 0, 0);
-#ifndef GT_NOPRIO
     __builtin_amdgcn_s_setprio(0);
-#endif
   };
   auto issue = [&](int p) {  // even phase p >= 2 issues slice p/2 - 1 + TNST
-#ifndef GT_NODMA  // diagnostics variant: the ring is filled once (wrong results, timing only)
     const int sidx = (p >> 1) - 1 + TNST;
     if (p >= 2 && sidx < nk) dma(sidx);
-#endif
   };
   auto wait_for = [&](int j) {  // end of phase 2j - 1: own pieces of slice j landed
     if (j >= nk) return;
@@ -194,9 +181,6 @@ __global__ __launch_bounds__(512, 1) void gemm_tile_kernel(const bf16* __restric
     }
   }
   __syncthreads();  // the ring is reused for the output tile
-#ifdef GT_NOEPI  // diagnostics variant: no epilogue (timing only)
-  if (acc[0][0][0] != 12345.f) return;
-#endif
 
   if constexpr (EPI == GT_BF16) {
     // C tile lane layout: row 16a + 4fg + r (of the wave's 128), column 16b + fr (of its 64)

@@ -215,13 +215,9 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
   __syncthreads();
   const int pos0 = (int)p.a_roff + l0;  // attention position of the wave's row 0
   for (int c = 0; c < nch; ++c) {
-#ifndef RG_NOSTAGE
     if (c + 1 < nch) stash((c + 1) & 1);
     if (c + 2 < nch) fetch(c + 2);
     const bf16* W = Ws + (c & 1) * QCEL;
-#else
-    const bf16* W = Ws;
-#endif
     const int n0 = c * QC, j = n0 / GE;  // 0 q, 1 k, 2 v
     const int h0 = (n0 - j * GE) >> 5;   // first of the chunk's two heads
     f32x4 acc[QC / 16][2];
@@ -278,9 +274,7 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
         }
       }
     }
-#ifndef RG_NOSYNC
     __syncthreads();
-#endif
   }
 }
 

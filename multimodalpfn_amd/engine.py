@@ -117,6 +117,7 @@ class HipEngine:
         self._streams: list = []
         self.lanes = DEFAULT_LANES
         self.batch = DEFAULT_BATCH
+        self.refs = 1  # model copies holding this engine (PerFeatureTransformer.__deepcopy__ shares it)
 
     # ------------------------------------------------------------------ plumbing
     def _stream(self) -> int:
@@ -127,6 +128,12 @@ class HipEngine:
 
     def _bind_stream(self) -> None:
         self._check(self.lib.mmpfn_set_stream(self.ctx, ctypes.c_void_p(self._stream())), "mmpfn_set_stream")
+
+    def release(self) -> None:
+        """Drop one holder's reference; the context is destroyed with the last one."""
+        self.refs -= 1
+        if self.refs <= 0:
+            self.close()
 
     def close(self) -> None:
         if getattr(self, "ctx", None):
@@ -146,7 +153,11 @@ class HipEngine:
 
     def _pos(self, n: int) -> torch.Tensor:
         if n not in self._pos_cache:
-            self._pos_cache[n] = pos_rand(self.cfg, n, self.device).to(self.device)
+            t = pos_rand(self.cfg, n, self.device).to(self.device)
+            # drawn / copied on whichever stream (lane) asked first, read later from every lane: wait for
+            # it here once, so no lane can read the cached table before it is complete
+            torch.cuda.current_stream(self.device).synchronize()
+            self._pos_cache[n] = t
         return self._pos_cache[n]
 
     # ------------------------------------------------------------------ compute
@@ -321,13 +332,21 @@ class HipEngine:
         outs: dict[int, torch.Tensor] = {}
         store: dict[int, tuple] = {}
 
-        def run(unit):
+        def run(unit, stream=None):
             if len(unit) == 1:
                 x, t, y = store[unit[0]]
                 outs[unit[0]] = self.forward(x, t, y, precision, check_nan=False)
             else:
                 for i, o in zip(unit, self.forward_batch([store[i] for i in unit], precision)):
                     outs[i] = o
+            if stream is not None:
+                # the unit's device inputs were made on the caller's stream (e.g. each member's
+                # torch.cat of train and test rows): keep their blocks from being reused before the
+                # lane's kernels have read them
+                for i in unit:
+                    for t in store[i]:
+                        if isinstance(t, torch.Tensor) and t.is_cuda:
+                            t.record_stream(stream)
             for i in unit:
                 del store[i]
 
@@ -344,9 +363,12 @@ class HipEngine:
                 run(unit)
             else:
                 k = launched % lanes
+                # the unit's inputs may have been produced on the caller's stream after the lanes forked
+                # (a generator builds each member just before its unit launches): order the lane behind it
+                streams[k].wait_stream(main)
                 with torch.cuda.stream(streams[k]):
                     self._check(self.lib.mmpfn_select_lane(self.ctx, k), "mmpfn_select_lane")
-                    run(unit)
+                    run(unit, streams[k])
                     if _DEBUG_SYNC:
                         torch.cuda.synchronize(self.device)
             launched += 1

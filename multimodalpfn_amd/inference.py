@@ -66,6 +66,16 @@ def _mixer_tokens(model, eng, image_train, image_test, prec: int, cache: dict | 
     return torch.cat([train, test], 0)
 
 
+def _n_mixer_tokens(model, image) -> int:
+    """Image tokens the mixer appends per row (C of SURVEY.md 8a: cap_heads for MGM+CAP, mgm_heads * n_mod
+    for MGM, the expert count for MoE)."""
+    if image is None or model.mixer_type not in ("MGM", "MGM+CAP", "MoE"):
+        return 0
+    n_mod = np.shape(image)[1] if np.ndim(image) == 3 else 1
+    cfg = model.cfg
+    return {"MGM": cfg.mgm_heads * n_mod, "MGM+CAP": cfg.cap_heads, "MoE": cfg.mgm_heads}[model.mixer_type]
+
+
 @dataclass
 class _Member:
     config: Any
@@ -95,8 +105,16 @@ class InferenceEngine:
 
         eng = model.engine(model._device() if device.type != "cuda" else device)
         prec = _precision(model, eng.device, autocast, forced_dtype)
-        mine, gather = member_shard(len(members), [self._member_cost(m, X, image_test) for m in members])
+        mine, gather = member_shard(len(members), [self._member_cost(m, X, image_test, model) for m in members],
+                                    keys=[self._member_key(m) for m in members], unit=eng.batch)
         cache = self._device_cache if self._cacheable else None
+        if cache is not None:
+            # device copies made with other weights (load_state_dict / invalidate_engine after fit) or by
+            # another engine are stale
+            tag = (model._weights_version, id(eng))
+            if cache.get("_tag") != tag:
+                cache.clear()
+                cache["_tag"] = tag
         tokens = _mixer_tokens(model, eng, image_train, image_test, prec, cache) if mine else None
         def items():  # a generator: forward_many launches each unit as soon as its members are ready
             for i in mine:
@@ -122,11 +140,20 @@ class InferenceEngine:
     _cacheable = True  # the members' train tables and train images are fixed after fit
 
     @staticmethod
-    def _member_cost(m: _Member, X, image_test) -> float:
+    def _member_cost(m: _Member, X, image_test, model) -> float:
+        from multimodalpfn_amd.parallel import member_cost
+
         n_tr = len(m.y_train)
         n_te = len(X) if X is not None else len(image_test)
+        fpg = model.features_per_group
         F = 0 if m.X_train is None else np.asarray(m.X_train).shape[1]
-        return float((F // 2 + 2) * (n_tr + n_te) * n_tr)
+        C = _n_mixer_tokens(model, image_test)
+        return member_cost((F + fpg - 1) // fpg + C + 1, n_tr + n_te, n_tr, model.cfg.emsize, model.cfg.nhid)
+
+    @staticmethod
+    def _member_key(m: _Member):
+        """Members the engine can stack into one batched forward share this key (same F and N)."""
+        return (None if m.X_train is None else np.asarray(m.X_train).shape[1], len(m.y_train))
 
 
 @dataclass

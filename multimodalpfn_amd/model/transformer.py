@@ -249,7 +249,11 @@ class PerFeatureTransformer(nn.Module):
         memo[id(self)] = new
         for k, v in self.__dict__.items():
             if k == "_engines":
-                new.__dict__[k] = v  # shared: same weights
+                # the engines are shared (same weights), the dict is not: each holder counts as one
+                # reference, so invalidating or re-keying one copy leaves the others' engines open
+                new.__dict__[k] = dict(v)
+                for eng in v.values():
+                    eng.refs += 1
             elif k == "_train_cache":
                 new.__dict__[k] = None
             else:
@@ -265,7 +269,7 @@ class PerFeatureTransformer(nn.Module):
     def invalidate_engine(self) -> None:
         """Drop packed device weights (call after modifying parameters in place)."""
         for eng in self._engines.values():
-            eng.close()
+            eng.release()
         self._engines.clear()
         self._weights_version += 1
 
@@ -329,7 +333,7 @@ class PerFeatureTransformer(nn.Module):
         if eng is None:
             for old in list(self._engines):
                 if old[0] == str(dev):
-                    self._engines.pop(old).close()
+                    self._engines.pop(old).release()
             eng = HipEngine(cfg, self.state_dict(), dev)
             self._engines[key] = eng
         return eng

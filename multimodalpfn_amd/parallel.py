@@ -3,8 +3,8 @@
 Members are independent forwards (``inference.py:294-349``); the only cross-member
 step is the softmax mean (``classifier.py:555-561``).  Each rank (one process per
 GPU, ``torch.distributed`` with the ``nccl`` backend = RCCL over xGMI) runs the
-members assigned to it by greedy longest-processing-time on the cost model
-``T_m * S * N`` and contributes its fixed-size logit block to ONE all-gather.
+members assigned to it by greedy longest-processing-time on the forward's flop model
+(``member_cost``; units of equal-geometry members kept together) and contributes its fixed-size logit block to ONE all-gather.
 There is no other collective on the data path.
 """
 
@@ -15,20 +15,36 @@ import heapq
 import torch
 
 
-def lpt_assign(costs: list[float], world: int) -> list[list[int]]:
-    """Greedy LPT: member indices per rank, heaviest first, to the least-loaded rank."""
+def lpt_assign(costs: list[float], world: int, keys: list | None = None, unit: int = 1) -> list[list[int]]:
+    """Greedy LPT: member indices per rank, heaviest first, to the least-loaded rank.
+
+    With ``keys`` (one geometry key per member) and ``unit > 1`` the members of one key are first cut
+    into units of ``unit`` (the engine's batched forward stacks exactly such members), and whole units
+    are assigned, so the per-rank batching the single-GPU scheduler relies on survives the split."""
+    if keys is None or unit <= 1:
+        groups = [[i] for i in range(len(costs))]
+    else:
+        by_key: dict = {}
+        for i, k in enumerate(keys):
+            by_key.setdefault(k, []).append(i)
+        groups = [ids[j : j + unit] for ids in by_key.values() for j in range(0, len(ids), unit)]
+    gcost = [sum(costs[i] for i in g) for g in groups]
     heap = [(0.0, r) for r in range(world)]
     heapq.heapify(heap)
     out: list[list[int]] = [[] for _ in range(world)]
-    for i in sorted(range(len(costs)), key=lambda i: (-costs[i], i)):
+    for gi in sorted(range(len(groups)), key=lambda g: (-gcost[g], groups[g][0])):
         load, r = heapq.heappop(heap)
-        out[r].append(i)
-        heapq.heappush(heap, (load + costs[i], r))
+        out[r].extend(groups[gi])
+        heapq.heappush(heap, (load + gcost[gi], r))
     return [sorted(x) for x in out]
 
 
-def member_cost(n_tokens: int, S: int, N: int) -> float:
-    return float(n_tokens) * S * N
+def member_cost(n_tokens: int, S: int, N: int, E: int = 192, FF: int = 768) -> float:
+    """Forward flops of one member per layer, up to a constant: per token the feature
+    and item QKV / out projections (16 E^2), the MLP (4 E FF), the feature attention over the row's
+    T tokens (4 T E) and the item attention against the N train rows (4 N E)."""
+    T = float(n_tokens)
+    return T * S * E * (16.0 * E + 4.0 * FF + 4.0 * N + 4.0 * T)
 
 
 def allgather_logits(local: torch.Tensor, assignment: list[list[int]], rank: int, group=None) -> torch.Tensor:
@@ -62,7 +78,7 @@ def allgather_logits(local: torch.Tensor, assignment: list[list[int]], rank: int
     return out
 
 
-def member_shard(n_members: int, costs: list[float], group=None):
+def member_shard(n_members: int, costs: list[float], group=None, keys: list | None = None, unit: int = 1):
     """This rank's members and a gather function for the classifier's member loop.
 
     Returns ``(mine, gather)``: ``mine`` lists the member indices this rank runs;
@@ -75,7 +91,7 @@ def member_shard(n_members: int, costs: list[float], group=None):
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
     world = dist.get_world_size(group) if multi else 1
     rank = dist.get_rank(group) if multi else 0
-    assignment = lpt_assign(costs, world) if multi else [list(range(n_members))]
+    assignment = lpt_assign(costs, world, keys, unit) if multi else [list(range(n_members))]
     mine = assignment[rank]
 
     def gather(outs: dict[int, torch.Tensor], device, Q: int, n_out: int) -> list[torch.Tensor]:

@@ -43,3 +43,20 @@ def rel_err(a, b) -> float:
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return float(np.abs(a - b).max() / max(1.0, np.abs(b).max()))
+
+
+def check_argmax(out, ref, min_agree: float, label: str = "") -> float:
+    """Argmax agreement of ``out`` with ``ref`` (rows x classes); prints every disagreeing row's
+    reference top-2 margin (a flip on a near-tie is rounding, a flip on a wide margin is a bug)."""
+    out = np.asarray(out, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    a, b = out.argmax(1), ref.argmax(1)
+    bad = np.nonzero(a != b)[0]
+    agree = 1.0 - len(bad) / max(1, len(a))
+    if len(bad):
+        srt = np.sort(ref, axis=1)
+        margins = srt[:, -1] - srt[:, -2]
+        print(f"{label}: argmax agreement {agree:.4f}; disagreeing rows (row, ref margin, out margin):",
+              [(int(i), float(margins[i]), float(out[i, a[i]] - out[i, b[i]])) for i in bad[:20]])
+    assert agree >= min_agree, (label, agree, min_agree)
+    return agree

@@ -76,3 +76,24 @@ def test_outlier_params_hook_like_reference():
     assert model._effective_config().remove_outliers_sigma == 7.0
     norm.remove_outliers = False
     assert model._effective_config().remove_outliers_sigma is None
+
+
+def test_loader_refuses_variant_builds(tmp_path, monkeypatch):
+    """A library carrying the variant marker (an A/B or stamps build) and any MMPFN_LIB override load
+    only under MMPFN_DIAGNOSTICS=1, so the product path cannot pick up a build with changed kernels."""
+    import shutil
+    import subprocess
+
+    from multimodalpfn_amd import _lib
+
+    src = tmp_path / "m.c"
+    src.write_text('const char *const mmpfn_variant_flags = "test: -DX";\n')
+    so = tmp_path / "libvar.so"
+    subprocess.run([shutil.which("gcc") or "gcc", "-shared", "-fPIC", str(src), "-o", str(so)], check=True)
+    monkeypatch.delenv("MMPFN_DIAGNOSTICS", raising=False)
+    with pytest.raises(RuntimeError, match="variant build"):
+        _lib.load_library(so)
+    monkeypatch.setenv("MMPFN_LIB", str(so))
+    monkeypatch.setattr(_lib, "_LIB", None)
+    with pytest.raises(RuntimeError, match="MMPFN_DIAGNOSTICS"):
+        _lib.load_library()

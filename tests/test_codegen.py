@@ -103,3 +103,26 @@ def test_mlp_eight_wave_option_does_not_spill():
     res = _resources("mlp_rows.hip", ["-DMLP_NW=8"])
     hits = {k: v for k, v in res.items() if "mlp_rows_kernelILi2ELb1ELi8E" in k}
     assert hits and max(hits.values()) == 0, hits
+
+
+ABLATIONS = re.compile(r"\b(A2_NO[A-Z]+|MLP_NO[A-Z0-9]+|RG_NO[A-Z]+|GT_NO[A-Z]+|A2_S?PRIO)\b")
+
+
+def test_product_sources_carry_no_ablation_switches():
+    """Timing ablations (switches that drop exps, stores, fills or barriers and give wrong results) are
+    not part of the product sources; A/B experiments live in local variant builds only."""
+    for src in sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp")) + sorted(CSRC.glob("*.h")):
+        hits = ABLATIONS.findall(src.read_text())
+        assert not hits, (src.name, sorted(set(hits)))
+
+
+def test_shipped_library_is_the_production_build():
+    """Variant builds export ``mmpfn_variant_flags`` (tools/build_variant*.sh, make dbg) and the loader
+    refuses them without MMPFN_DIAGNOSTICS=1; the in-tree library must not carry the marker."""
+    lib = CSRC.parent / "libmmpfn_hip.so"
+    if not lib.exists():
+        pytest.skip("library not built")
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    syms = subprocess.run([nm, "-D", "--defined-only", str(lib)], capture_output=True, text=True, check=True).stdout
+    assert "mmpfn_variant_flags" not in syms
+    assert "mmpfn_forward" in syms

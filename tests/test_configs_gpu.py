@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import oracle_spec, rel_err, torch_sd
+from helpers import check_argmax, oracle_spec, rel_err, torch_sd
 from oracle.forward import oracle_forward
 
 pytestmark = pytest.mark.gpu
@@ -29,7 +29,7 @@ S_ROWS, N_TRAIN, N_FEAT, N_CAT, N_CLS = 2298, 1838, 21, 18, 6
 # name -> (mgm heads, cap heads, modalities, data seed)
 FULL = {"C": (64, 24, 1, 2), "C-mgm256": (256, 24, 1, 2), "D": (64, 24, 2, 3)}
 BF16_BAND = {"C": 3.5e-2, "C-mgm256": 3.5e-2, "D": 2e-2}  # measured 1.64e-2, 1.77e-2, 0.99e-2
-BF16_AGREE = {"C": 0.97, "C-mgm256": 0.97, "D": 0.97}
+BF16_AGREE = {"C": 0.995, "C-mgm256": 0.995, "D": 0.995}  # measured 1.00 on all three
 
 
 def _model(cfg, sd):
@@ -86,7 +86,7 @@ def test_full_size_config_matches_oracle(name):
     assert e32 <= F32_TOL, (name, e32)
     assert (f32.argmax(1) == ref.argmax(1)).all()
     assert eb <= BF16_BAND[name], (name, eb)
-    assert agree >= BF16_AGREE[name], (name, agree)
+    check_argmax(b16, ref, BF16_AGREE[name], f"bf16 {name}")
 
 
 def _ragged_members(n, seed, tok_n):

@@ -51,8 +51,8 @@ def _worker(rank, world, port, ckdir, q):
 
         shares, orig = [], par.member_shard
 
-        def recording(n, costs, group=None):  # the members this rank actually forwards
-            mine, gather = orig(n, costs, group)
+        def recording(n, costs, group=None, **kw):  # the members this rank actually forwards
+            mine, gather = orig(n, costs, group, **kw)
             shares.append((n, list(mine)))
             return mine, gather
 

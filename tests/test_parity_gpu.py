@@ -2,7 +2,7 @@
 
 Tolerances (north star: fp32 logits within 1e-4 relative, argmax bit-exact):
   fp32 parity mode : max|d logits| <= 1e-4 * max(1, max|ref|), argmax identical
-  bf16 perf mode   : max|d logits| <= 2e-2 * max(1, max|ref|) (about 2x the measured worst), argmax >= 95 %
+  bf16 perf mode   : max|d logits| <= 2e-2 * max(1, max|ref|) (about 2x the measured worst), argmax agreement >= 99.5 % (measured 100 % on every case)
 """
 
 import math
@@ -11,13 +11,14 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import CASES, load_case, oracle_spec, rel_err, torch_sd
+from helpers import CASES, check_argmax, load_case, oracle_spec, rel_err, torch_sd
 from oracle.forward import layer_forward, oracle_forward
 
 pytestmark = pytest.mark.gpu
 
 F32_TOL = 1e-4
 LARGE_BF16_TOL = {"B": 2.5e-2, "E": 3.5e-2}  # measured 1.28e-2 and 1.80e-2 (profiles/r02)
+BF16_AGREE = 0.995  # argmax agreement; measured 1.00 on every golden and on B / E (profiles/r02)
 BF16_TOL = 2e-2  # measured 3.1e-3 .. 9.5e-3 over the goldens (profiles/r02/pytest_gpu_r02a.log)
 
 
@@ -56,10 +57,9 @@ def test_forward_bf16_close_to_reference(case):
     out = run_case(z, make_model(cfg, sd), autocast=True)
     assert np.isfinite(out).all()
     err = rel_err(out, z["logits"])
-    agree = (out.argmax(1) == z["logits"].argmax(1)).mean()
-    print(f"bf16 {case}: rel err {err:.3e}, argmax agreement {agree:.3f}")
+    print(f"bf16 {case}: rel err {err:.3e}")
     assert err <= BF16_TOL, err
-    assert agree >= 0.95, agree
+    check_argmax(out, z["logits"], BF16_AGREE, f"bf16 {case}")
 
 
 def test_embedding_and_layer_taps_fp32():
@@ -299,6 +299,63 @@ def test_forward_lanes_match_sequential(lanes, batch):
         assert torch.equal(a.cpu(), b.cpu())
 
 
+def test_forward_many_generator_of_fresh_device_tensors():
+    """``predict_proba``'s call form: ``forward_many`` pulls a generator whose members are built on the
+    caller's stream AFTER the lanes forked (torch.cat of the train and test rows, then the caller goes
+    on allocating and writing).  Lanes must order behind each member's producer and keep its blocks
+    alive until they have read them: lanes=2 == lanes=1, bitwise."""
+    from synth import synth_image, synth_labels, synth_state_dict, synth_table
+
+    from multimodalpfn_amd import _lib
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    cfg = ModelConfig(nlayers=3, mgm_heads=8, cap_heads=4)
+    sd = synth_state_dict(state_dict_spec(cfg), 5)
+    model = make_model(cfg, sd)
+    eng = model.engine()
+    S, N, F = 1200, 900, 12
+    x = synth_table(S, F, 5, n_cat=3)
+    im = torch.from_numpy(synth_image(S, 1, 5)).cuda()
+    y = synth_labels(S, 3, 5)[:N]
+    tok = eng.mixer_tokens(im, _lib.PREC_BF16)
+    perms = [np.random.default_rng(m).permutation(F) for m in range(6)]
+
+    def gen():
+        for p in perms:
+            xp = torch.from_numpy(np.ascontiguousarray(x[:, p]))
+            x_full = torch.cat([xp[:N].cuda(), xp[N:].cuda()], 0)  # made on the caller's stream
+            yield x_full, tok, y
+            del x_full
+            junk = torch.empty((S, F), device="cuda").fill_(float("nan"))  # reuses freed blocks
+            junk.mul_(2.0)
+
+    with torch.inference_mode():
+        ref = eng.forward_many(list(gen()), _lib.PREC_BF16, lanes=1, batch=1)
+        torch.cuda.synchronize()
+        for lanes, batch in [(2, 1), (2, 2)]:
+            par = eng.forward_many(gen(), _lib.PREC_BF16, lanes=lanes, batch=batch)
+            eng.status()
+            for a, b in zip(ref, par):
+                assert torch.equal(a.cpu(), b.cpu()), (lanes, batch)
+
+
+def test_deepcopy_keeps_the_original_engine():
+    """``deepcopy(model)`` shares the packed weights; re-loading weights into the copy must not close
+    the original's engine (InferenceEngineCacheKV keeps one model copy per member)."""
+    import copy
+
+    z, meta, cfg, sd = load_case("pad_ufes_12l")
+    model = make_model(cfg, sd)
+    before = run_case(z, model)
+    other = copy.deepcopy(model)
+    assert run_case(z, other).tolist() == before.tolist()  # shared engine, same weights
+    sd2 = {k: v * 0.5 if k.endswith("mlp.linear2.weight") else v for k, v in torch_sd(sd).items()}
+    other.load_state_dict(sd2)
+    changed = run_case(z, other)
+    assert not np.array_equal(changed, before)
+    np.testing.assert_array_equal(run_case(z, model), before)
+
+
 def test_forward_batch_fp32_matches_reference():
     """fp32 parity mode through the batched forward (members stacked) against the goldens."""
     from multimodalpfn_amd import _lib
@@ -346,10 +403,10 @@ def test_large_config_matches_oracle_on_device(name, S, N, F, n_cls, seed):
     assert np.isfinite(f32).all() and np.isfinite(b16).all()
     assert rel_err(f32, ref) <= F32_TOL, (name, rel_err(f32, ref))
     assert (f32.argmax(1) == ref.argmax(1)).all()
-    eb, agree = rel_err(b16, ref), float((b16.argmax(1) == ref.argmax(1)).mean())
-    print(f"bf16 {name}: rel err {eb:.3e}, argmax agreement {agree:.4f}; fp32 rel err {rel_err(f32, ref):.3e}")
+    eb = rel_err(b16, ref)
+    print(f"bf16 {name}: rel err {eb:.3e}; fp32 rel err {rel_err(f32, ref):.3e}")
     assert eb <= LARGE_BF16_TOL[name[0]], (name, eb)
-    assert agree >= 0.95, agree
+    check_argmax(b16, ref, BF16_AGREE, f"bf16 {name}")
 
 
 @pytest.mark.parametrize("prec", [0, 1])

@@ -9,7 +9,7 @@ LIB=${1:-}
 cd /tmp || exit 1
 pass() {
   local name=$1; shift
-  MMPFN_LIB=$LIB timeout -s KILL 90 rocprofv3 --pmc "$@" -d $R/gpurun_out/attn_sq/$name -o run --output-format csv -- \
+  MMPFN_DIAGNOSTICS=1 MMPFN_LIB=$LIB timeout -s KILL 90 rocprofv3 --pmc "$@" -d $R/gpurun_out/attn_sq/$name -o run --output-format csv -- \
     python3 $R/tools/attn_time.py 5 > $R/gpurun_out/attn_sq/$name.log 2>&1
 }
 pass a SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT || exit 1

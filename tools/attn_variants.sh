@@ -17,6 +17,6 @@ else
   shift
   mkdir -p gpurun_out
   for name in "$@"; do
-    MMPFN_LIB=multimodalpfn_amd/libmmpfn_var_$name.so timeout -k 10 120 python3 tools/attn_time.py 50 || exit 1
+    MMPFN_DIAGNOSTICS=1 MMPFN_LIB=multimodalpfn_amd/libmmpfn_var_$name.so timeout -k 10 120 python3 tools/attn_time.py 50 || exit 1
   done
 fi

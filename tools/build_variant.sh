@@ -12,4 +12,6 @@ for src in capi.cpp gemm.hip attention.hip encoder.hip mixer.hip mlp.hip mlp_row
     $extra $flags -x hip -c $C/$src -o $B/$src.o &
 done
 wait
+printf 'const char *const mmpfn_variant_flags = "%s";\n' "$name: $flags" > $B/variant_marker.c
+gcc -fPIC -c $B/variant_marker.c -o $B/variant_marker.o || exit 1
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o multimodalpfn_amd/libmmpfn_var_$name.so $B/*.o && echo built $name

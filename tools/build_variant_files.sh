@@ -11,4 +11,6 @@ for src in "$@"; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -mllvm -amdgpu-mfma-vgpr-form=1 \
     $extra $flags -x hip -c $C/$src -o $B/$src.o || exit 1
 done
+printf 'const char *const mmpfn_variant_flags = "%s";\n' "$name: $flags" > $B/variant_marker.c
+gcc -fPIC -c $B/variant_marker.c -o $B/variant_marker.o || exit 1
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o multimodalpfn_amd/libmmpfn_var_$name.so $B/*.o && echo built $name

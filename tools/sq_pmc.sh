@@ -4,7 +4,7 @@ set -o pipefail
 R=$PWD; mkdir -p gpurun_out; export TMPDIR=/tmp
 LIB=${1:-}
 cd /tmp || exit 1
-MMPFN_LIB=$LIB timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_MFMA \
+MMPFN_DIAGNOSTICS=1 MMPFN_LIB=$LIB timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_MFMA \
   -d $R/gpurun_out/sqpmc -o run --output-format csv -- python3 $R/tools/prof_forward.py 1 > $R/gpurun_out/sqpmc.log 2>&1 || exit 1
 cd $R && python3 - <<'PY'
 import csv, collections

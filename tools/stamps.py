@@ -8,6 +8,7 @@ import os
 import subprocess
 import sys
 
+os.environ.setdefault("MMPFN_DIAGNOSTICS", "1")
 os.environ.setdefault("MMPFN_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                 "multimodalpfn_amd", "libmmpfn_hip_dbg.so"))
 import tools_prof_forward  # noqa: E402

@@ -19,7 +19,7 @@ else
   shift
   R=$PWD; mkdir -p gpurun_out; export TMPDIR=/tmp
   for name in "$@"; do
-    cd /tmp && MMPFN_LIB=$R/multimodalpfn_amd/libmmpfn_var_$name.so timeout -k 10 200 rocprofv3 --kernel-trace --stats \
+    cd /tmp && MMPFN_DIAGNOSTICS=1 MMPFN_LIB=$R/multimodalpfn_amd/libmmpfn_var_$name.so timeout -k 10 200 rocprofv3 --kernel-trace --stats \
       -d $R/gpurun_out/var_$name -o run --output-format csv -- python3 $R/tools/prof_forward.py 2 > $R/gpurun_out/var_$name.log 2>&1 || exit 1
     cd $R && echo "== $name" && python3 tools/kstats.py gpurun_out/var_$name/run_kernel_stats.csv 5
   done
