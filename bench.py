@@ -598,8 +598,13 @@ def main():
         dt32 = timed_steps(step32, k32, 1, world, device)
         f32 = {"value": round(M * S_ROWS * k32 / dt32, 1), "unit": "rows/s", "ms_per_step": round(dt32 / k32 * 1e3, 3),
                "steps": k32, "dtype": "f32",
-               "note": "the same step in the fp32 parity mode (fp32-input MFMA everywhere; logits within 1e-4 "
-                       "of the oracle)"}
+               "note": "the same step in the fp32 parity mode (MMPFN_PREC_F32: fp32 tensors, every contraction on "
+                       "bf16 MFMA with split hi + lo operands, three products; logits within 1e-4 of the oracle)"}
+        stepm = make_step(eng, members, mine, assignment, rank, img, _lib.PREC_F32_MFMA, args.lanes, args.batch)
+        dtm = timed_steps(stepm, 3, 1, world, device)
+        f32["fp32_input_mfma_mode"] = {
+            "value": round(M * S_ROWS * 3 / dtm, 1), "unit": "rows/s", "ms_per_step": round(dtm / 3 * 1e3, 3),
+            "note": "MMPFN_PREC_F32_MFMA: the same step on fp32-input MFMA (exact fp32 fma chains)"}
 
     api = api_def = None
     if args.api_steps > 0:

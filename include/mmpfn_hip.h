@@ -49,8 +49,10 @@ extern "C" {
 #define MMPFN_ERR_STATE (-4)     /* call order (weights not finalised, ...) */
 #define MMPFN_ERR_WEIGHT (-5)    /* missing / mis-shaped weight */
 
-#define MMPFN_PREC_F32 0  /* parity mode: fp32 everywhere (fp32-input MFMA) */
-#define MMPFN_PREC_BF16 1 /* performance mode: bf16 MFMA operands, fp32 accumulate / residual / LN */
+#define MMPFN_PREC_F32 0      /* parity mode: fp32 tensors; contractions on bf16 MFMA with every operand split into
+                                  bf16 hi + lo planes (hi.hi + hi.lo + lo.hi, fp32 accumulate: ~2^-16 relative) */
+#define MMPFN_PREC_BF16 1     /* performance mode: bf16 MFMA operands, fp32 accumulate / residual / LN */
+#define MMPFN_PREC_F32_MFMA 2 /* parity mode on fp32-input MFMA (exact fp32 fma chains, 1/16 of the bf16 rate) */
 
 #define MMPFN_MIXER_NONE 0
 #define MMPFN_MIXER_MGM 1

@@ -21,8 +21,14 @@ MMPFN_ERR_NAN = -3
 MMPFN_ERR_STATE = -4
 MMPFN_ERR_WEIGHT = -5
 
-PREC_F32 = 0
-PREC_BF16 = 1
+PREC_F32 = 0       # parity mode: split-bf16 three-product MFMAs (fp32 operands to 2^-16), fp32 softmax / LN
+PREC_BF16 = 1      # performance mode (the reference's fp16 autocast counterpart)
+PREC_F32_MFMA = 2  # parity mode on fp32-input MFMA (exact fp32 fma chains, 1/16 of the bf16 rate)
+
+
+def f32_precision() -> int:
+    """Engine code of an fp32 forward: PREC_F32, or PREC_F32_MFMA under ``MMPFN_F32_MODE=mfma``."""
+    return PREC_F32_MFMA if os.environ.get("MMPFN_F32_MODE", "").lower() == "mfma" else PREC_F32
 
 MIXER_NONE, MIXER_MGM, MIXER_MGM_CAP, MIXER_MOE = 0, 1, 2, 3
 MIXER_CODES = {"MGM": MIXER_MGM, "MGM+CAP": MIXER_MGM_CAP, "MoE": MIXER_MOE, None: MIXER_NONE}

@@ -846,6 +846,318 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 #endif
 }
 
+// ------------------------------------------------------------------ item attention, parity mode
+// PREC_F32: attn_item2's task map, LDS images and fixed-reference softmax on fp32 Q / K / V^T, every
+// operand split into bf16 hi + lo planes (x = hi + lo to 2^-17): Q in registers, K / V^T as they are
+// staged into LDS (two planes per image), and P = exp2(S) in registers.  Per 64-key tile and chain
+//   S^T = Kl Qh + Kh Ql + Kh Qh          (6 x v_mfma_f32_32x32x16_bf16 per 32 keys)
+//   O^T += Vl Ph + Vh Pl + Vh Ph,  l += 1.(Pl + Ph)  (selector MFMAs over both P planes)
+// in fp32 accumulators: each product carries the operands to 2^-16, so the attention matches the
+// exact fp32 softmax to ~1e-5 relative at three bf16 MFMAs where fp32-input MFMA takes sixteen.
+// Output O is fp32 ([row][H*32], the out-projection's A).
+constexpr int A3_NCH = 2;
+constexpr int A3_QPW = 32 * A3_NCH;
+constexpr int A3_QPB = A2_NW * A3_QPW;
+constexpr int A3_STAGE = 4 * 4096;  // K hi | K lo | V^T hi | V^T lo
+
+__device__ __forceinline__ void a3_split8(f32x4 a, f32x4 b, float sc, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x = a[i] * sc, y = b[i] * sc;
+    hi[i] = (bf16)x, hi[4 + i] = (bf16)y;
+    lo[i] = (bf16)(x - (float)hi[i]), lo[4 + i] = (bf16)(y - (float)hi[4 + i]);
+  }
+}
+
+// exact two-pass softmax for one query per lane, fp32 K / V^T straight from global memory
+__device__ __attribute__((noinline)) void a3_exact_rows(const Attn2Args& p, const float* Kg, const float* Vg,
+                                                         const float* qrow, float* orow, bool valid, float c) {
+  float q[32], o[32];
+#pragma unroll
+  for (int d = 0; d < 32; ++d) q[d] = qrow[d] * c, o[d] = 0.f;
+  float m = -INFINITY;
+  for (int k = 0; k < p.nk; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) s = fmaf(q[d], Kg[(int64_t)k * 32 + d], s);
+    m = fmaxf(m, s);
+  }
+  float l = 0.f;
+  for (int k = 0; k < p.nk; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) s = fmaf(q[d], Kg[(int64_t)k * 32 + d], s);
+    const float e = exp2f(s - m);
+    l += e;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) o[d] = fmaf(e, Vg[(int64_t)d * p.Npad + k], o[d]);
+  }
+  if (valid) {
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int d = 0; d < 32; d += 4) *(f32x4*)(orow + d) = f32x4{o[d] * inv, o[d + 1] * inv, o[d + 2] * inv, o[d + 3] * inv};
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2][A3_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+
+  int b, g, chunk;  // task map of attn_item2 (contiguous task ranges per XCD)
+  {
+    const int nbk = p.nblocks, pid = blockIdx.x;
+    const int xcd = pid & 7, slot = pid >> 3;
+    const int task = xcd * (nbk >> 3) + min(xcd, nbk & 7) + slot;
+    b = task / p.tasks_per_b;
+    const int rem = task - b * p.tasks_per_b;
+    g = 0;
+    int base = p.tstart[0];
+#pragma unroll
+    for (int h = 1; h < 9; ++h)
+      if (h < p.H && p.tstart[h] <= rem) g = h, base = p.tstart[h];
+    chunk = rem - base;
+  }
+  const int cnt = p.na + (g == p.kvb ? p.H * p.nb : 0);
+  const int jw = chunk * A3_QPB + wave * A3_QPW;
+  const bool active = jw < cnt;
+
+  const int64_t kvoff = (int64_t)b * p.kv_bstride + (int64_t)g * p.Npad * 32;
+  const float* Kg = (const float*)p.k + kvoff;
+  const float* Vg = (const float*)p.vt + kvoff;
+  const float c = p.q_prescaled ? 1.0f : kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
+
+  int qh[A3_NCH], qsrow[A3_NCH];
+  bool qok[A3_NCH];
+  bf16x8 qfh[A3_NCH][2], qfl[A3_NCH][2];
+#pragma unroll
+  for (int qb = 0; qb < A3_NCH; ++qb) {
+    const int j = jw + 32 * qb + r;
+    qok[qb] = j < cnt;
+    const int jc = min(j, cnt - 1);
+    if (jc < p.na) {
+      qh[qb] = g, qsrow[qb] = p.a0 + jc;
+    } else {
+      const int jj = jc - p.na;
+      qh[qb] = jj / p.nb, qsrow[qb] = p.b0 + jj % p.nb;
+    }
+    const float* qrow = (const float*)p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      a3_split8(*(const f32x4*)(qrow + 16 * ks + 8 * hh), *(const f32x4*)(qrow + 16 * ks + 8 * hh + 4), c,
+                qfh[qb][ks], qfl[qb][ks]);
+  }
+
+  const int ntiles = (p.nk + A2_KT - 1) / A2_KT;
+  const bool partial = (p.nk % A2_KT) != 0;
+
+  // staging: 8 fp32 of one K row and 8 fp32 of one V^T row per thread and tile
+  const int krow = tid >> 2, kc = tid & 3;
+  const int vd = tid >> 3, vc = tid & 7;
+  f32x4 rk[2], rv[2];
+  auto gload = [&](int t) {
+    const int k0 = t * A2_KT;
+    const float* ks = Kg + (int64_t)(k0 + krow) * 32 + kc * 8;
+    const float* vs = Vg + (int64_t)vd * p.Npad + k0 + vc * 8;
+    rk[0] = *(const f32x4*)ks, rk[1] = *(const f32x4*)(ks + 4);
+    rv[0] = *(const f32x4*)vs, rv[1] = *(const f32x4*)(vs + 4);
+    if (partial && t == ntiles - 1) {  // keys >= nk: V = 0 so that p = 0 never meets NaN / inf padding
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (k0 + vc * 8 + j >= p.nk) rv[j >> 2][j & 3] = 0.f;
+    }
+  };
+  const int koff_w = a2_koff(krow, kc);
+  const int voff_w0 = a2_voff(vd, vc & ~1) + 8 * (vc & 1), voff_w1 = a2_voff(vd, vc | 1) + 8 * (vc & 1);
+  auto lstore = [&](int buf) {
+    unsigned char* Ks = lds[buf];
+    bf16x8 hi, lo;
+    a3_split8(rk[0], rk[1], 1.0f, hi, lo);
+    *(bf16x8*)(Ks + koff_w) = hi;
+    *(bf16x8*)(Ks + 4096 + koff_w) = lo;
+    a3_split8(rv[0], rv[1], 1.0f, hi, lo);
+    const u32x4 vh = __builtin_bit_cast(u32x4, hi), vl = __builtin_bit_cast(u32x4, lo);
+    *(u32x2*)(Ks + 8192 + voff_w0) = u32x2{vh.x, vh.y};
+    *(u32x2*)(Ks + 8192 + voff_w1) = u32x2{vh.z, vh.w};
+    *(u32x2*)(Ks + 12288 + voff_w0) = u32x2{vl.x, vl.y};
+    *(u32x2*)(Ks + 12288 + voff_w1) = u32x2{vl.z, vl.w};
+  };
+  int kro[2][2], vro[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      kro[u][i] = a2_koff(32 * u + r, 2 * i + hh);
+      vro[u][i] = 8192 + a2_voff(r, 2 * (2 * u + i) + hh);
+    }
+  bf16x8 sel;  // row-sum selector (attn_item2)
+  {
+    const int m = lane & 15, kg = lane >> 4;
+    const bool one = (m == 0 && (kg & 1) == 0) || (m == 1 && (kg & 1) == 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sel[j] = (bf16)(one ? 1.0f : 0.0f);
+  }
+  f32x16 o[A3_NCH];
+  f32x4 lacc[A3_NCH];
+  float mref[A3_NCH];
+#pragma unroll
+  for (int qb = 0; qb < A3_NCH; ++qb) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[qb][i] = 0.f;
+    lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mref[qb] = 0.f;
+  }
+
+  auto tile = [&](int it, auto maskc, auto firstc, auto refc) {
+    constexpr bool MASK = decltype(maskc)::value;
+    constexpr bool FIRST = decltype(firstc)::value;
+    constexpr bool REF = decltype(refc)::value;
+    const f32x16 zero16 = {};
+    const int k0 = it * A2_KT;
+    if (it + 1 < ntiles) gload(it + 1);
+    const unsigned char* Ks = lds[it & 1];
+    if (active) {
+      bf16x8 kh[2][2], kl[2][2], vh[2][2], vl[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          kh[u][i] = *(const bf16x8*)(Ks + kro[u][i]);
+          kl[u][i] = *(const bf16x8*)(Ks + 4096 + kro[u][i]);
+          vh[u][i] = *(const bf16x8*)(Ks + vro[u][i]);
+          vl[u][i] = *(const bf16x8*)(Ks + 4096 + vro[u][i]);
+        }
+      f32x16 s[A3_NCH][2];
+#pragma unroll
+      for (int qb = 0; qb < A3_NCH; ++qb)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[u][0], qfh[qb][0], zero16, 0, 0, 0);
+          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[u][1], qfh[qb][1], s[qb][u], 0, 0, 0);
+          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[u][0], qfl[qb][0], s[qb][u], 0, 0, 0);
+          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[u][1], qfl[qb][1], s[qb][u], 0, 0, 0);
+          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[u][0], qfh[qb][0], s[qb][u], 0, 0, 0);
+          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[u][1], qfh[qb][1], s[qb][u], 0, 0, 0);
+        }
+      if constexpr (MASK) {
+#pragma unroll
+        for (int qb = 0; qb < A3_NCH; ++qb)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (k0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * hh >= p.nk) s[qb][u][i] = -INFINITY;
+      }
+      if constexpr (FIRST) {
+#pragma unroll
+        for (int qb = 0; qb < A3_NCH; ++qb) {
+          float m = fmaxf(s[qb][0][0], s[qb][1][0]);
+#pragma unroll
+          for (int i = 1; i < 16; ++i) m = fmaxf(m, fmaxf(s[qb][0][i], s[qb][1][i]));
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+          mref[qb] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        }
+      }
+      if constexpr (REF) {
+#pragma unroll
+        for (int qb = 0; qb < A3_NCH; ++qb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            s[qb][0][i] -= mref[qb];
+            s[qb][1][i] -= mref[qb];
+          }
+      }
+#pragma unroll
+      for (int qb = 0; qb < A3_NCH; ++qb)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp) {
+            bf16x8 ph, pl;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float e = __builtin_amdgcn_exp2f(s[qb][u][8 * sp + j]);
+              ph[j] = (bf16)e;
+              pl[j] = (bf16)(e - (float)ph[j]);
+            }
+            o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl[u][sp], ph, o[qb], 0, 0, 0);
+            o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[u][sp], pl, o[qb], 0, 0, 0);
+            o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[u][sp], ph, o[qb], 0, 0, 0);
+            lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pl, lacc[qb], 0, 0, 0);
+            lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, ph, lacc[qb], 0, 0, 0);
+          }
+    }
+    if (it + 1 < ntiles) lstore((it + 1) & 1);
+    __syncthreads();
+  };
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  using Y = std::true_type;
+  using N = std::false_type;
+  auto pass = [&](auto wmc) {
+    constexpr bool WM = decltype(wmc)::value;
+    using F = std::integral_constant<bool, WM>;
+    if (ntiles == 1) {
+      if (partial) tile(0, Y{}, F{}, F{});
+      else tile(0, N{}, F{}, F{});
+    } else {
+      tile(0, N{}, F{}, F{});
+      const int nfull = p.nk / A2_KT;
+      for (int it = 1; it < nfull; ++it) tile(it, N{}, N{}, F{});
+      if (partial) tile(nfull, Y{}, N{}, F{});
+    }
+  };
+  auto rowsum = [&](int qb) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(lacc[qb][0]), __float_as_uint(lacc[qb][1]),
+                                                    false, false);
+    const auto s2 = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);
+    return __uint_as_float(s2[0]);
+  };
+  pass(N{});
+  {  // reference-free pass out of [2^-60, 2^100) for any query of the block: re-run with the first tile's max
+    bool bad = false;
+    if (active)
+#pragma unroll
+      for (int qb = 0; qb < A3_NCH; ++qb) {
+        const unsigned lb = __float_as_uint(rowsum(qb)) & 0x7fffffffu;
+        bad |= lb >= 0x71800000u || lb < 0x21800000u;
+      }
+    if (__syncthreads_or(bad ? 1 : 0)) {
+#pragma unroll
+      for (int qb = 0; qb < A3_NCH; ++qb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[qb][i] = 0.f;
+        lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      gload(0);
+      lstore(0);
+      __syncthreads();
+      pass(Y{});
+    }
+  }
+  if (!active) return;
+#pragma unroll
+  for (int qb = 0; qb < A3_NCH; ++qb) {
+    const float ls = rowsum(qb);
+    float* orow = (float*)p.o + ((int64_t)b * p.S + qsrow[qb]) * (p.H * 32) + qh[qb] * 32;
+    if (__any((__float_as_uint(ls) & 0x7fffffffu) >= 0x71800000u)) {
+      const float* qrow = (const float*)p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
+      a3_exact_rows(p, Kg, Vg, qrow, orow, qok[qb] && hh == 0, c);
+      continue;
+    }
+    const float inv = 1.0f / ls;
+    if (qok[qb]) {
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq)
+        *(f32x4*)(orow + 8 * gq + 4 * hh) = f32x4{o[qb][4 * gq] * inv, o[qb][4 * gq + 1] * inv,
+                                                  o[qb][4 * gq + 2] * inv, o[qb][4 * gq + 3] * inv};
+    }
+  }
+}
+
 }  // namespace
 
 #ifdef A2_STAMPS
@@ -854,9 +1166,10 @@ extern "C" int mmpfn_dbg_attn_stamps(void* host) {
 }
 #endif
 
-hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
-                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride,
-                             bool q_prescaled) {
+namespace {
+hipError_t launch_item_attention(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
+                                 int Npad, int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st,
+                                 int64_t kv_bstride, bool q_prescaled, bool x3) {
   if (na + nb <= 0 || T <= 0) return hipSuccess;
   if (nk <= 0 || Npad % A2_KT != 0 || nk > Npad || H > 8 || H <= 0) return hipErrorInvalidValue;
   if (nb > 0 && (kvb < 0 || kvb >= H)) return hipErrorInvalidValue;
@@ -870,22 +1183,41 @@ hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void*
   if (getenv("A2_STAMPS_PRESCALED")) a.q_prescaled = 1;
 #endif
   if (kv_bstride > 0 && (na > 0 || kvb != 0)) return hipErrorInvalidValue;  // cache layout holds head 0 only
+  const int qpb = x3 ? A3_QPB : A2_QPB;
   int acc = 0;
   for (int g = 0; g < H; ++g) {
     a.tstart[g] = acc;
     const int cnt = na + (g == a.kvb ? H * nb : 0);
-    acc += (cnt + A2_QPB - 1) / A2_QPB;
+    acc += (cnt + qpb - 1) / qpb;
   }
   for (int g = H; g < 9; ++g) a.tstart[g] = acc;
   a.tasks_per_b = acc;
   a.nblocks = acc * T;
   if (a.nblocks == 0) return hipSuccess;
+  if (x3) {
+    hipLaunchKernelGGL(attn_item3_kernel, dim3(a.nblocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
 #ifdef MMPFN_ATTN_FP8PV
   hipLaunchKernelGGL(attn_item2_kernel<true>, dim3(a.nblocks), dim3(256), 0, st, a);
 #else
   hipLaunchKernelGGL(attn_item2_kernel<false>, dim3(a.nblocks), dim3(256), 0, st, a);
 #endif
   return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
+                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride,
+                             bool q_prescaled) {
+  return launch_item_attention(q, k, vt, out, S, T, H, Npad, nk, a0, na, b0, nb, kvb, st, kv_bstride, q_prescaled,
+                               false);
+}
+
+hipError_t launch_attn_item3(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
+                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride) {
+  return launch_item_attention(q, k, vt, out, S, T, H, Npad, nk, a0, na, b0, nb, kvb, st, kv_bstride, false, true);
 }
 
 hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int nw, hipStream_t st) {
@@ -913,9 +1245,12 @@ hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* 
   if (kv_bstride > 0 && kv_head_fixed != 0) return hipErrorInvalidValue;
   a.o_bstride = S, a.o_qstride = 1;
   a.s0 = s0, a.nq = nq, a.nk = nk, a.kvh_fixed = kv_head_fixed, a.H = H;
-  if (prec == PREC_BF16) {
-    if (kv_head_fixed < 0) return launch_attn_item2(q, k, vt, out, S, T, H, Npad, nk, s0, nq, 0, 0, -1, st, kv_bstride);
-    return launch_attn_item2(q, k, vt, out, S, T, H, Npad, nk, 0, 0, s0, nq, kv_head_fixed, st, kv_bstride);
+  if (prec == PREC_BF16 || prec == PREC_F32) {
+    const bool x3 = prec == PREC_F32;
+    if (kv_head_fixed < 0)
+      return launch_item_attention(q, k, vt, out, S, T, H, Npad, nk, s0, nq, 0, 0, -1, st, kv_bstride, false, x3);
+    return launch_item_attention(q, k, vt, out, S, T, H, Npad, nk, 0, 0, s0, nq, kv_head_fixed, st, kv_bstride, false,
+                                 x3);
   }
   return launch_attn(a, T, prec, 4, st);
 }

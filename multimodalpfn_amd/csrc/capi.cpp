@@ -27,6 +27,7 @@ namespace {
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  size_t n = 0;  // elements (split weight planes: elements per plane)
 };
 
 struct LayerW {  // packed per layer, [N][K] row-major
@@ -70,6 +71,8 @@ struct mmpfn_ctx {
   std::vector<DevBuf> owned;
 
   std::vector<LayerW> layers;
+  // parity mode (PREC_F32): every GEMM weight also as bf16 hi | lo planes, keyed by its fp32 copy
+  std::map<const void*, DevBuf> split;
   DevBuf enc_w, y_w, y_b, pe_w, pe_b, dec_w1, dec_b1, dec_w2, dec_b2;
   // mixer
   DevBuf mgm_w1, mgm_w1_h, mgm_b1, mgm_w2, mgm_w2_h, mgm_b2;
@@ -251,10 +254,31 @@ std::vector<float> pack_feat_rows(const std::vector<float>& qkv, const std::vect
   return o;
 }
 
+// bf16 hi | lo planes of v (hi = bf16(w), lo = bf16(w - hi)), the weight operand of the parity mode's
+// three-product GEMMs, stored under the key of its fp32 copy f
+int upsplit(mmpfn_ctx* ctx, const DevBuf& f, const std::vector<float>& v) {
+  std::vector<uint16_t> h(2 * v.size());
+  for (size_t i = 0; i < v.size(); ++i) {
+    const uint16_t hi = f2bf(v[i]);
+    uint32_t u = (uint32_t)hi << 16;
+    float fh;
+    std::memcpy(&fh, &u, 4);
+    h[i] = hi;
+    h[v.size() + i] = f2bf(v[i] - fh);
+  }
+  DevBuf& b = ctx->split[f.p];
+  int rc = ensure(ctx, b, h.size() * 2);
+  if (rc) return rc;
+  b.n = v.size();
+  HIPCHK(hipMemcpy(b.p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  return MMPFN_OK;
+}
+
 int up2(mmpfn_ctx* ctx, DevBuf& f, DevBuf& h, const std::vector<float>& v) {
   int rc = upload(ctx, f, v, false);
   if (rc) return rc;
-  return upload(ctx, h, v, true);
+  if ((rc = upload(ctx, h, v, true))) return rc;
+  return upsplit(ctx, f, v);
 }
 
 // fold a preceding LayerNorm affine (g, b over K inputs) into Linear (W [N][K], c [N])
@@ -289,8 +313,10 @@ int finalize(mmpfn_ctx* ctx) {
         return rc;
     if ((rc = up2(ctx, L.item_out, L.item_out_h, transpose_out(*io, HD, E)))) return rc;
     if ((rc = upload(ctx, L.mlp1, *m1, false))) return rc;
+    if ((rc = upsplit(ctx, L.mlp1, *m1))) return rc;
     if ((rc = upload(ctx, L.mlp1_h, E == 192 ? pack_mlp1_perm(*m1, E, Fh) : *m1, true))) return rc;
     if ((rc = upload(ctx, L.mlp2, *m2, false))) return rc;
+    if ((rc = upsplit(ctx, L.mlp2, *m2))) return rc;
     if ((rc = upload(ctx, L.mlp2_h, pack_mlp2_perm(*m2, E, Fh), true))) return rc;
     std::vector<float> wtrain((size_t)3 * HD * E), wtest((size_t)HD * E);
     if (d.two_sets_of_queries) {
@@ -306,6 +332,8 @@ int finalize(mmpfn_ctx* ctx) {
     }
     if ((rc = upload(ctx, L.item_qkv, wtrain, false))) return rc;
     if ((rc = upload(ctx, L.item_qtest, wtest, false))) return rc;
+    if ((rc = upsplit(ctx, L.item_qkv, wtrain))) return rc;
+    if ((rc = upsplit(ctx, L.item_qtest, wtest))) return rc;
     // bf16 copies: the Q rows carry the attention kernel's log2(e)/sqrt(32) (attn_item2 with
     // q_prescaled: no per-query scaling pass; one bf16 rounding of Q instead of two)
     const float qsc = 1.4426950408889634f / std::sqrt((float)(E / d.nhead));
@@ -456,7 +484,20 @@ int finalize(mmpfn_ctx* ctx) {
   return MMPFN_OK;
 }
 
-inline const void* W(const DevBuf& f, const DevBuf& h, int prec) { return prec == PREC_BF16 ? h.p : f.p; }
+// weight operand of launch_gemm in a precision mode: bf16 copy, fp32 copy (PREC_F32_MFMA), or the
+// hi | lo planes of the parity mode with the offset of the lo plane
+void setw(const mmpfn_ctx* ctx, GemmArgs& a, const DevBuf& f, const DevBuf& h, int prec) {
+  a.w_lo_off = 0;
+  if (prec == PREC_BF16) {
+    a.W = h.p;
+  } else if (prec == PREC_F32) {
+    const auto it = ctx->split.find(f.p);
+    a.W = it == ctx->split.end() ? nullptr : it->second.p;
+    a.w_lo_off = it == ctx->split.end() ? 0 : (int64_t)it->second.n;
+  } else {
+    a.W = f.p;
+  }
+}
 
 GemmArgs gargs() {
   GemmArgs a;
@@ -483,7 +524,7 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
   if (S <= 0 || N <= 0 || N > S || (x && F <= 0) || C < 0 || U <= 0)
     return fail(ctx, MMPFN_ERR_INVALID, "bad forward geometry");
   if (!x && C == 0) return fail(ctx, MMPFN_ERR_INVALID, "no input tokens");
-  if (prec != PREC_F32 && prec != PREC_BF16) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  if (prec != PREC_F32 && prec != PREC_BF16 && prec != PREC_F32_MFMA) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   const int E = d.emsize, fpg = d.features_per_group;
   const int G = x ? (F + fpg - 1) / fpg : 0;
   const int T = G + C + 1;
@@ -496,7 +537,8 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
     RC(ensure(ctx, ctx->ws_X, (size_t)M * R * E * 4));
     RC(ensure(ctx, ctx->ws_O, (size_t)M * R * E * 4));
     const size_t Tpad = (T + 63) / 64 * 64;
-    const size_t big = std::max(R * E + (size_t)2 * S * Tpad * E, (size_t)M * (R * E + (size_t)2 * T * Npad * E)) * 4;
+    size_t big = std::max(R * E + (size_t)2 * S * Tpad * E, (size_t)M * (R * E + (size_t)2 * T * Npad * E)) * 4;
+    if (prec == PREC_F32) big = std::max(big, (size_t)M * R * d.nhid * 4);  // the parity-mode MLP's hidden rows
     RC(ensure(ctx, ctx->ws_big, big));
     RC(ensure(ctx, ctx->ws_pe, (size_t)(G + C + 1) * E * 4));
     RC(ensure(ctx, ctx->ws_slots, (size_t)(G + 1) * fpg * sizeof(SlotParams)));
@@ -591,7 +633,7 @@ int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int S, int T, in
     GemmArgs a = gargs();
     // logical rows m = s*T + t: A row t*S + s; scatter batch b = s, position t
     a.A = X, a.lda = E, a.a_rdiv = T, a.a_rmul = 1, a.a_rmul2 = S;
-    a.W = W(L.feat_qkv, L.feat_qkv_h, prec);
+    setw(ctx, a, L.feat_qkv, L.feat_qkv_h, prec);
     a.M = (int)R, a.N = 3 * E, a.K = E;
     a.q = Qf, a.k = Kf, a.v = Vf, a.S = T, a.Npad = Tpad, a.T = T, a.H = H;
     HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
@@ -603,7 +645,7 @@ int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int S, int T, in
     f.s0 = 0, f.nq = T, f.nk = T, f.kvh_fixed = -1, f.H = H;
     HIPCHK(launch_attn(f, S, prec, 1, st));
     GemmArgs b = gargs();
-    b.A = O, b.lda = E, b.W = W(L.feat_out, L.feat_out_h, prec);
+    b.A = O, b.lda = E, setw(ctx, b, L.feat_out, L.feat_out_h, prec);
     b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
     HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
   }
@@ -639,7 +681,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
     } else {
       GemmArgs c = gargs();
       c.A = Xall, c.lda = E, c.a_rdiv = S, c.a_rmul = S, c.a_roff = 0;
-      c.W = W(L.item_qtest, L.item_qtest_h, prec);
+      setw(ctx, c, L.item_qtest, L.item_qtest_h, prec);
       c.M = TM * S, c.N = E, c.K = E;
       c.q = Qi, c.k = Ki, c.v = Vi, c.S = S, c.Npad = Npad, c.T = TM, c.H = H;
       HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
@@ -657,14 +699,14 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
     } else {
       GemmArgs a = gargs();
       a.A = Xall, a.lda = E, a.a_rdiv = N, a.a_rmul = S, a.a_roff = 0;
-      a.W = W(L.item_qkv, L.item_qkv_h, prec);
+      setw(ctx, a, L.item_qkv, L.item_qkv_h, prec);
       a.M = TM * N, a.N = 3 * E, a.K = E;
       a.q = Qi, a.k = Ki, a.v = Vi, a.S = S, a.Npad = Npad, a.T = TM, a.H = H;
       HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
       if (Q > 0) {
         GemmArgs c = a;
         c.a_rdiv = Q, c.a_roff = N;
-        c.W = W(L.item_qtest, L.item_qtest_h, prec);
+        setw(ctx, c, L.item_qtest, L.item_qtest_h, prec);
         c.M = TM * Q, c.N = E;
         HIPCHK(launch_gemm(c, prec, EPI_ITEM_QKV, true, !bf, 1, st));
       }
@@ -693,6 +735,8 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
       }
       HIPCHK(launch_attn_item2(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st, 0, true));
       if (ev) HIPCHK(hipEventRecord(ev[1], st));
+    } else if (prec == PREC_F32) {  // parity mode: split-bf16 products, train and test rows in one launch
+      HIPCHK(launch_attn_item3(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st));
     } else {
       HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, 0, N, N, -1, prec, st));
       if (Q > 0) HIPCHK(launch_attn_item(Qi, Ki, Vi, O, S, TM, H, Npad, N, Q, N, 0, prec, st));
@@ -703,7 +747,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
     HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, RM, Xall, d.ln_eps, st));
   } else {
     GemmArgs b = gargs();
-    b.A = O, b.lda = E, b.W = W(L.item_out, L.item_out_h, prec);
+    b.A = O, b.lda = E, setw(ctx, b, L.item_out, L.item_out_h, prec);
     b.M = (int)RM, b.N = E, b.K = E, b.X = Xall, b.ln_eps = d.ln_eps;
     HIPCHK(launch_gemm(b, prec, EPI_RES_LN, !bf, true, 1, st));
   }
@@ -716,11 +760,27 @@ bool mlp_fuses_out(const mmpfn_model_desc& d, int prec) { return prec == PREC_BF
 // ---- MLP (mlp.py:93-104) + residual + LN over RM tokens; O non-null: the fused out-projection first
 int mlp_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int64_t RM, int prec, const void* O) {
   const mmpfn_model_desc& d = ctx->d;
-  if (mlp_fuses_out(d, prec))  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders
+  if (mlp_fuses_out(d, prec)) {  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders
     HIPCHK(launch_mlp_rows(Xall, L.mlp1_h.p, L.mlp2_h.p, RM, d.emsize, d.nhid, d.ln_eps, ctx->stream, O,
                            O ? L.item_out_h.p : nullptr));
-  else
-    HIPCHK(launch_mlp_fused(Xall, L.mlp1.p, L.mlp2.p, RM, d.emsize, d.nhid, d.ln_eps, PREC_F32, ctx->stream));
+  } else if (prec == PREC_F32) {
+    // parity mode: up-projection + GELU(erf) and down-projection + residual + LN as two split-bf16 GEMMs,
+    // the hidden rows [RM][nhid] fp32 in the (by now free) attention scratch
+    RC(ensure(ctx, ctx->ws_big, (size_t)RM * d.nhid * 4));
+    float* Hd = (float*)ctx->ws_big.p;
+    GemmArgs u = gargs();
+    u.A = Xall, u.lda = d.emsize, u.act = ACT_GELU;
+    setw(ctx, u, L.mlp1, L.mlp1_h, prec);
+    u.M = (int)RM, u.N = d.nhid, u.K = d.emsize, u.C = Hd, u.ldc = d.nhid;
+    HIPCHK(launch_gemm(u, prec, EPI_STORE, true, true, 1, ctx->stream));
+    GemmArgs dn = gargs();
+    dn.A = Hd, dn.lda = d.nhid;
+    setw(ctx, dn, L.mlp2, L.mlp2_h, prec);
+    dn.M = (int)RM, dn.N = d.emsize, dn.K = d.nhid, dn.X = Xall, dn.ln_eps = d.ln_eps;
+    HIPCHK(launch_gemm(dn, prec, EPI_RES_LN, true, true, 1, ctx->stream));
+  } else {
+    HIPCHK(launch_mlp_fused(Xall, L.mlp1.p, L.mlp2.p, RM, d.emsize, d.nhid, d.ln_eps, PREC_F32_MFMA, ctx->stream));
+  }
   return MMPFN_OK;
 }
 
@@ -770,7 +830,7 @@ int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* mtok,
   RC(ensure(ctx, ctx->mx[1], (size_t)rows * mg * (D / 2) * eb));  // GLU output
   HIPCHK(launch_layernorm_rows(image, rows, D, 1e-5f, ctx->mx[0].p, !bf, nullptr, nullptr, st));
   GemmArgs a = gargs();
-  a.A = ctx->mx[0].p, a.lda = D, a.W = W(ctx->mgm_w1, ctx->mgm_w1_h, prec), a.bias = (const float*)ctx->mgm_b1.p;
+  a.A = ctx->mx[0].p, a.lda = D, setw(ctx, a, ctx->mgm_w1, ctx->mgm_w1_h, prec), a.bias = (const float*)ctx->mgm_b1.p;
   a.M = (int)rows, a.N = mg * D, a.K = D, a.C = ctx->mx[1].p, a.ldc = (int64_t)mg * (D / 2);
   if (bf && (mg * D) % 256 == 0 && D % 64 == 0)
     HIPCHK(launch_gemm_glu_big(ctx->mx[0].p, a.W, a.bias, ctx->mx[1].p, (int)rows, mg * D, D, st));
@@ -778,7 +838,7 @@ int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* mtok,
     HIPCHK(launch_gemm(a, prec, EPI_GLU, !bf, !bf, 1, st));
   GemmArgs b = gargs();
   b.A = ctx->mx[1].p, b.lda = (int64_t)mg * (D / 2), b.a_zstride = D / 2;
-  b.W = W(ctx->mgm_w2, ctx->mgm_w2_h, prec), b.w_zstride = (int64_t)E * (D / 2);
+  setw(ctx, b, ctx->mgm_w2, ctx->mgm_w2_h, prec), b.w_zstride = (int64_t)E * (D / 2);
   b.bias = (const float*)ctx->mgm_b2.p, b.b_zstride = E;
   b.M = (int)rows, b.N = E, b.K = D / 2;
   b.C = mtok, b.ldc = E, b.rdiv2 = n_mod, b.rmul2 = M, b.zmul = n_mod;
@@ -806,7 +866,7 @@ int mixer_cap(mmpfn_ctx* ctx, const float* mtok, int S, int M, float* tokens, in
   } else {
     HIPCHK(launch_layernorm_rows(mtok, srows, E, 1e-5f, ctx->mx[3].p, !bf, nullptr, nullptr, st));
     GemmArgs c = gargs();
-    c.A = ctx->mx[3].p, c.lda = E, c.W = W(ctx->cap_kv, ctx->cap_kv_h, prec), c.bias = (const float*)ctx->cap_kv_b.p;
+    c.A = ctx->mx[3].p, c.lda = E, setw(ctx, c, ctx->cap_kv, ctx->cap_kv_h, prec), c.bias = (const float*)ctx->cap_kv_b.p;
     c.M = (int)srows, c.N = 2 * E, c.K = E, c.C = ctx->mx[4].p, c.ldc = 2 * E;
     HIPCHK(launch_gemm(c, prec, EPI_STORE, !bf, !bf, 1, st));
   }
@@ -815,16 +875,16 @@ int mixer_cap(mmpfn_ctx* ctx, const float* mtok, int S, int M, float* tokens, in
   const int64_t crow = (int64_t)S * cap;
   // projections run in fp32 A (tiny); bf16 weights in perf mode
   GemmArgs o = gargs();
-  o.A = ctx->mx[5].p, o.lda = E, o.W = W(ctx->cap_o, ctx->cap_o_h, prec), o.bias = (const float*)ctx->cap_o_b.p;
+  o.A = ctx->mx[5].p, o.lda = E, setw(ctx, o, ctx->cap_o, ctx->cap_o_h, prec), o.bias = (const float*)ctx->cap_o_b.p;
   o.M = (int)crow, o.N = E, o.K = E, o.C = ctx->mx[6].p, o.ldc = E;
   HIPCHK(launch_gemm(o, prec, EPI_STORE, true, true, 1, st));
   GemmArgs f0 = gargs();
-  f0.A = ctx->mx[6].p, f0.lda = E, f0.W = W(ctx->cap_f0, ctx->cap_f0_h, prec);
+  f0.A = ctx->mx[6].p, f0.lda = E, setw(ctx, f0, ctx->cap_f0, ctx->cap_f0_h, prec);
   f0.bias = (const float*)ctx->cap_f0_b.p, f0.act = ACT_GELU;
   f0.M = (int)crow, f0.N = 2 * E, f0.K = E, f0.C = ctx->mx[7].p, f0.ldc = 2 * E;
   HIPCHK(launch_gemm(f0, prec, EPI_STORE, true, true, 1, st));
   GemmArgs f3 = gargs();
-  f3.A = ctx->mx[7].p, f3.lda = 2 * E, f3.W = W(ctx->cap_f3, ctx->cap_f3_h, prec);
+  f3.A = ctx->mx[7].p, f3.lda = 2 * E, setw(ctx, f3, ctx->cap_f3, ctx->cap_f3_h, prec);
   f3.bias = (const float*)ctx->cap_f3_b.p;
   f3.M = (int)crow, f3.N = E, f3.K = 2 * E, f3.C = ctx->mx[5].p, f3.ldc = E;  // reuse mx5 for ffn out
   HIPCHK(launch_gemm(f3, prec, EPI_STORE, true, true, 1, st));
@@ -863,12 +923,12 @@ int mixer(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, i
     }
     HIPCHK(launch_layernorm_rows(x0, S, D, 1e-5f, ctx->mx[0].p, !bf, nullptr, nullptr, st));
     GemmArgs a = gargs();
-    a.A = ctx->mx[0].p, a.lda = D, a.W = W(ctx->moe_w1, ctx->moe_w1_h, prec), a.bias = (const float*)ctx->moe_b1.p;
+    a.A = ctx->mx[0].p, a.lda = D, setw(ctx, a, ctx->moe_w1, ctx->moe_w1_h, prec), a.bias = (const float*)ctx->moe_b1.p;
     a.act = ACT_GELU, a.M = S, a.N = ne * (D / 2), a.K = D, a.C = ctx->mx[1].p, a.ldc = (int64_t)ne * (D / 2);
     HIPCHK(launch_gemm(a, prec, EPI_STORE, !bf, !bf, 1, st));
     GemmArgs b = gargs();
     b.A = ctx->mx[1].p, b.lda = (int64_t)ne * (D / 2), b.a_zstride = D / 2;
-    b.W = W(ctx->moe_w2, ctx->moe_w2_h, prec), b.w_zstride = (int64_t)E * (D / 2);
+    setw(ctx, b, ctx->moe_w2, ctx->moe_w2_h, prec), b.w_zstride = (int64_t)E * (D / 2);
     b.bias = (const float*)ctx->moe_b2.p, b.b_zstride = E;
     b.M = S, b.N = E, b.K = D / 2, b.C = tokens, b.ldc = E, b.rdiv2 = 1, b.rmul2 = ne, b.zmul = 1;
     HIPCHK(launch_gemm(b, prec, EPI_REMAP, !bf, true, ne, st));
@@ -923,6 +983,7 @@ void mmpfn_destroy(mmpfn_ctx* ctx) {
                     &ctx->ws_flag})
     fr(*b);
   for (auto& b : ctx->mx) fr(b);
+  for (auto& kv : ctx->split) fr(kv.second);
   for (auto& L : ctx->lanes)
     for (DevBuf* b : {&L.ws_X, &L.ws_O, &L.ws_big, &L.ws_pe, &L.ws_slots, &L.ws_scr, &L.ws_flag}) fr(*b);
   delete ctx;
@@ -1214,7 +1275,8 @@ static int tap_check(mmpfn_ctx* ctx, int layer, const void* X, int precision) {
   if (!ctx || !X) return MMPFN_ERR_INVALID;
   if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
   if (layer < 0 || layer >= ctx->d.nlayers) return fail(ctx, MMPFN_ERR_INVALID, "bad layer index");
-  if (precision != PREC_F32 && precision != PREC_BF16) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  if (precision != PREC_F32 && precision != PREC_BF16 && precision != PREC_F32_MFMA)
+    return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
   return MMPFN_OK;
 }
@@ -1245,7 +1307,8 @@ int mmpfn_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* token
   if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
   if (ctx->d.mixer_type != MMPFN_MIXER_MGM && ctx->d.mixer_type != MMPFN_MIXER_MGM_CAP)
     return fail(ctx, MMPFN_ERR_INVALID, "model has no MGM head bank");
-  if (precision != PREC_F32 && precision != PREC_BF16) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  if (precision != PREC_F32 && precision != PREC_BF16 && precision != PREC_F32_MFMA)
+    return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
   return mixer_mgm(ctx, image, S, n_mod, tokens, precision);
 }
@@ -1254,7 +1317,8 @@ int mmpfn_cap(mmpfn_ctx* ctx, const float* mgm_tokens, int S, int M, float* toke
   if (!ctx || !mgm_tokens || !tokens || S <= 0 || M <= 0) return MMPFN_ERR_INVALID;
   if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
   if (ctx->d.mixer_type != MMPFN_MIXER_MGM_CAP) return fail(ctx, MMPFN_ERR_INVALID, "model has no CAP");
-  if (precision != PREC_F32 && precision != PREC_BF16) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  if (precision != PREC_F32 && precision != PREC_BF16 && precision != PREC_F32_MFMA)
+    return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
   return mixer_cap(ctx, mgm_tokens, S, M, tokens, precision);
 }

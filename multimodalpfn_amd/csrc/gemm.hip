@@ -11,7 +11,9 @@
 // slices (64 bf16 or 32 f32), with the next slice's global loads in flight while
 // the current one is consumed (register staging, issue-early / write-late).
 //   bf16 path : v_mfma_f32_16x16x32_bf16, fp32 accumulate
-//   f32  path : v_mfma_f32_16x16x4_f32 (exact fp32 fma chain; parity mode)
+//   x3   path : parity mode (PREC_F32): A (fp32) split into bf16 hi + lo planes as it is staged,
+//               W pre-split on the host; acc += Ah.Wh + Ah.Wl + Al.Wh on v_mfma_f32_16x16x32_bf16
+//   f32  path : v_mfma_f32_16x16x4_f32 (exact fp32 fma chain; PREC_F32_MFMA)
 // A may be stored fp32 while the bf16 path computes: it is converted when written
 // to LDS, so the fp32 residual stream is never materialised in bf16 in HBM.
 #include "common.h"
@@ -25,6 +27,7 @@ constexpr int BM = 64;
 constexpr int BN = 192;
 constexpr int ROWB = 160;  // LDS bytes per staged row: 128 data + 32 pad (32 mod 64: conflict-free ds_read_b128)
 constexpr int LDS_STAGE = (BM + BN) * ROWB;
+constexpr int LDS_STAGE_X3 = 2 * (BM + BN) * ROWB;  // hi and lo planes of A and W
 constexpr int LN_STRIDE = 196;  // floats per row of the LayerNorm epilogue buffer
 constexpr int LDS_LN = BM * LN_STRIDE * 4;
 constexpr int A_CHUNKS = BM * 8 / 256;  // 16-byte LDS chunks per thread
@@ -36,11 +39,26 @@ struct Stage {
   static constexpr int AWORDS = (BF16 && AF32) ? 2 : 1;
 };
 
-template <bool BF16, bool AF32, bool OF32, int EPI>
+// hi = bf16(x), lo = bf16(x - hi): x = hi + lo to 2^-17 relative (parity mode)
+__device__ __forceinline__ void split8(const f32x4& f0, const f32x4& f1, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    hi[i] = (bf16)f0[i], hi[4 + i] = (bf16)f1[i];
+    lo[i] = (bf16)(f0[i] - (float)hi[i]), lo[4 + i] = (bf16)(f1[i] - (float)hi[4 + i]);
+  }
+}
+
+// MODE 0: fp32-input MFMA, 1: bf16, 2: x3 (split bf16, A fp32)
+template <int MODE, bool AF32, bool OF32, int EPI>
 __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
+  constexpr bool BF16 = MODE != 0;
+  constexpr bool X3 = MODE == 2;
+  static_assert(!X3 || AF32, "x3 splits an fp32 A");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* As = smem;
-  unsigned char* Ws = smem + BM * ROWB;
+  unsigned char* Ws = smem + (X3 ? 2 : 1) * BM * ROWB;
+  unsigned char* Asl = smem + BM * ROWB;          // x3: A lo plane
+  unsigned char* Wsl = Ws + BN * ROWB;            // x3: W lo plane
   typedef typename std::conditional<OF32, float, bf16>::type TO;
   constexpr int EB = BF16 ? 2 : 4;       // compute element bytes
   constexpr int BK = 128 / EB;           // K per staged slice
@@ -75,6 +93,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
 
   u32x4 ra[A_CHUNKS][AW];
   u32x4 rw[W_CHUNKS];
+  u32x4 rwl[X3 ? W_CHUNKS : 1];
 
   auto load_tile = [&](int k0) {
 #pragma unroll
@@ -97,6 +116,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
       const int c = tid + 256 * i;
       const int r = c >> 3, ch = c & 7;
       rw[i] = *(const u32x4*)(Wbase + ((int64_t)(n0 + r) * K + k0 + ch * (16 / EB)) * EB);
+      if constexpr (X3) rwl[i] = *(const u32x4*)(Wbase + (p.w_lo_off + (int64_t)(n0 + r) * K + k0 + ch * 8) * 2);
     }
   };
 
@@ -106,7 +126,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
       const int c = tid + 256 * i;
       const int r = c >> 3;
       u32x4 v;
-      if (BF16 && AF32) {
+      if constexpr (X3) {
+        bf16x8 hi, lo;
+        split8(__builtin_bit_cast(f32x4, ra[i][0]), __builtin_bit_cast(f32x4, ra[i][AW - 1]), hi, lo);
+        v = __builtin_bit_cast(u32x4, hi);
+        *(u32x4*)(Asl + r * ROWB + ach[i] * 16) = __builtin_bit_cast(u32x4, lo);
+      } else if (BF16 && AF32) {
         const f32x4 f0 = __builtin_bit_cast(f32x4, ra[i][0]);
         const f32x4 f1 = __builtin_bit_cast(f32x4, ra[i][AW - 1]);
         bf16x8 b;
@@ -122,6 +147,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
     for (int i = 0; i < W_CHUNKS; ++i) {
       const int c = tid + 256 * i;
       *(u32x4*)(Ws + (c >> 3) * ROWB + (c & 7) * 16) = rw[i];
+      if constexpr (X3) *(u32x4*)(Wsl + (c >> 3) * ROWB + (c & 7) * 16) = rwl[i];
     }
   };
 
@@ -141,7 +167,27 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
     const int fr = lane & 15, fg = lane >> 4;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      if constexpr (BF16) {
+      if constexpr (X3) {
+        bf16x8 af[2], afl[2], bw[6], bwl[6];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          af[mt] = *(const bf16x8*)(As + (wm * 32 + mt * 16 + fr) * ROWB + ks * 64 + fg * 16);
+          afl[mt] = *(const bf16x8*)(Asl + (wm * 32 + mt * 16 + fr) * ROWB + ks * 64 + fg * 16);
+        }
+#pragma unroll
+        for (int nt = 0; nt < 6; ++nt) {
+          bw[nt] = *(const bf16x8*)(Ws + (wn * 96 + nt * 16 + fr) * ROWB + ks * 64 + fg * 16);
+          bwl[nt] = *(const bf16x8*)(Wsl + (wn * 96 + nt * 16 + fr) * ROWB + ks * 64 + fg * 16);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 6; ++nt) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[mt], bw[nt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bwl[nt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bw[nt], acc[mt][nt], 0, 0, 0);
+          }
+      } else if constexpr (BF16) {
         bf16x8 af[2], bw[6];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
@@ -327,24 +373,30 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
   }
 }
 
-template <bool BF16, bool AF32, bool OF32, int EPI>
+template <int MODE, bool AF32, bool OF32, int EPI>
 hipError_t launch_t(const GemmArgs& a, int groups, hipStream_t st) {
   dim3 grid((a.M + BM - 1) / BM, a.N / BN, groups);
   constexpr int OUTB = (EPI == EPI_RES_LN || OF32) ? 4 : 2;
   constexpr int STAGED = EPI == EPI_RES_LN ? LDS_LN : BM * (BN + 16 / OUTB) * OUTB;
-  const int lds = STAGED > LDS_STAGE ? STAGED : LDS_STAGE;
-  hipLaunchKernelGGL((gemm_kernel<BF16, AF32, OF32, EPI>), grid, dim3(256), lds, st, a);
+  constexpr int STAGE = MODE == 2 ? LDS_STAGE_X3 : LDS_STAGE;
+  const int lds = STAGED > STAGE ? STAGED : STAGE;
+  if (lds > 65536) {  // x3: 80 KB of hi / lo planes
+    static const hipError_t attr = hipFuncSetAttribute((const void*)gemm_kernel<MODE, AF32, OF32, EPI>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (attr != hipSuccess) return attr;
+  }
+  hipLaunchKernelGGL((gemm_kernel<MODE, AF32, OF32, EPI>), grid, dim3(256), lds, st, a);
   return hipGetLastError();
 }
 
-template <bool BF16, bool AF32, bool OF32>
+template <int MODE, bool AF32, bool OF32>
 hipError_t launch_e(const GemmArgs& a, int epi, int groups, hipStream_t st) {
   switch (epi) {
-    case EPI_STORE: return launch_t<BF16, AF32, OF32, EPI_STORE>(a, groups, st);
-    case EPI_ITEM_QKV: return launch_t<BF16, AF32, OF32, EPI_ITEM_QKV>(a, groups, st);
-    case EPI_RES_LN: return launch_t<BF16, AF32, true, EPI_RES_LN>(a, groups, st);
-    case EPI_GLU: return launch_t<BF16, AF32, OF32, EPI_GLU>(a, groups, st);
-    case EPI_REMAP: return launch_t<BF16, AF32, OF32, EPI_REMAP>(a, groups, st);
+    case EPI_STORE: return launch_t<MODE, AF32, OF32, EPI_STORE>(a, groups, st);
+    case EPI_ITEM_QKV: return launch_t<MODE, AF32, OF32, EPI_ITEM_QKV>(a, groups, st);
+    case EPI_RES_LN: return launch_t<MODE, AF32, true, EPI_RES_LN>(a, groups, st);
+    case EPI_GLU: return launch_t<MODE, AF32, OF32, EPI_GLU>(a, groups, st);
+    case EPI_REMAP: return launch_t<MODE, AF32, OF32, EPI_REMAP>(a, groups, st);
   }
   return hipErrorInvalidValue;
 }
@@ -480,16 +532,20 @@ hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool ou
                        hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.N % BN != 0) return hipErrorInvalidValue;
-  if (prec == PREC_F32) {
+  if (prec == PREC_F32_MFMA) {
     if (!a_f32 || !out_f32) return hipErrorInvalidValue;
     if (a.K % 32 != 0) return hipErrorInvalidValue;
-    return launch_e<false, true, true>(a, epi, groups, st);
+    return launch_e<0, true, true>(a, epi, groups, st);
   }
   if (a.K % 64 != 0) return hipErrorInvalidValue;
-  if (a_f32) {
-    return out_f32 ? launch_e<true, true, true>(a, epi, groups, st) : launch_e<true, true, false>(a, epi, groups, st);
+  if (prec == PREC_F32) {  // x3: fp32 A split while staged, W given as hi | lo planes (w_lo_off)
+    if (!a_f32 || !out_f32 || a.w_lo_off <= 0) return hipErrorInvalidValue;
+    return launch_e<2, true, true>(a, epi, groups, st);
   }
-  return out_f32 ? launch_e<true, false, true>(a, epi, groups, st) : launch_e<true, false, false>(a, epi, groups, st);
+  if (a_f32) {
+    return out_f32 ? launch_e<1, true, true>(a, epi, groups, st) : launch_e<1, true, false>(a, epi, groups, st);
+  }
+  return out_f32 ? launch_e<1, false, true>(a, epi, groups, st) : launch_e<1, false, false>(a, epi, groups, st);
 }
 
 hipError_t launch_gemm_glu_big(const void* A, const void* W, const float* bias, void* C, int M, int N, int K,

@@ -5,7 +5,11 @@
 
 namespace mmpfn {
 
-enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1 };
+// PREC_F32 (parity mode): every large contraction on bf16 MFMA with both operands split into
+// bf16 hi + lo planes, x = hi + lo to 2^-17, and the three significant products hi.hi + hi.lo +
+// lo.hi accumulated in fp32 (the dropped lo.lo term is 2^-16 relative) -- 3 bf16 MFMAs at 16x the
+// fp32-input rate; PREC_F32_MFMA: the same forward on fp32-input MFMA (exact fp32 fma chains)
+enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1, PREC_F32_MFMA = 2 };
 
 enum Epi : int {
   EPI_STORE = 0,      // C[row] = act(acc + bias)
@@ -24,8 +28,9 @@ struct GemmArgs {
   int64_t lda;
   int64_t a_rdiv, a_rmul, a_rmul2, a_roff;
   int64_t a_zstride;  // elements between groups (blockIdx.z)
-  const void* W;      // [N][K] compute dtype, row-major
+  const void* W;      // [N][K] compute dtype, row-major (PREC_F32: the bf16 hi plane)
   int64_t w_zstride;
+  int64_t w_lo_off;   // PREC_F32: elements from W to its bf16 lo plane
   const float* bias;  // [N] or null
   int64_t b_zstride;
   int M, N, K;
@@ -122,6 +127,9 @@ hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int waves_per_b
 hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0,
                              bool q_prescaled = false);  // Q already scaled by log2(e)/sqrt(32)
+// parity mode (PREC_F32) of launch_attn_item2 on fp32 Q / K / V^T (split bf16 three-product MFMAs), fp32 O
+hipError_t launch_attn_item3(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
+                             int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0);
 // item attention: queries s in [s0, s0+nq), keys [0, nk); kv_head_fixed >= 0 forces that KV head
 hipError_t launch_attn_item(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
                             int Npad, int s0, int nq, int nk, int kv_head_fixed, int prec, hipStream_t st,

@@ -2,8 +2,9 @@
 
 Inputs are the oracle's own intermediate states of a golden case (so each tap is checked in
 isolation), plus config-C-sized states for the kernels' production shapes.  Tolerances:
-fp32 parity mode <= 2e-5 relative to max(1, max|ref|) per sublayer (the oracle runs fp64);
-bf16 mode <= 2e-2 (bf16 operands, fp32 accumulation / LayerNorm).
+fp32 parity mode (prec 0: split-bf16 three-product MFMAs) <= 5e-5 relative to max(1, max|ref|) per
+sublayer (the oracle runs fp64); fp32-input MFMA mode (prec 2) <= 2e-5; bf16 mode <= 2e-2 (bf16
+operands, fp32 accumulation / LayerNorm).
 """
 
 import pytest
@@ -14,7 +15,7 @@ from oracle.forward import embed_inputs, feat_sublayer, item_sublayer, mlp_subla
 
 pytestmark = pytest.mark.gpu
 
-TOL = {0: 2e-5, 1: 2e-2}
+TOL = {0: 5e-5, 1: 2e-2, 2: 2e-5}
 
 
 def _engine(cfg, sd):
@@ -37,7 +38,7 @@ def _golden_states(case):
     return cfg, sd, spec, {k: v.double() for k, v in w.items()}, X0, len(y), im
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 @pytest.mark.parametrize("case", ["mgmcap_edge", "pad_ufes_12l", "two_queries"])
 def test_layer_sublayer_taps_match_oracle(case, prec):
     cfg, sd, spec, w, X0, N, _ = _golden_states(case)
@@ -55,7 +56,7 @@ def test_layer_sublayer_taps_match_oracle(case, prec):
         X0 = Xm
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 @pytest.mark.parametrize("case", ["mgmcap_edge", "mgm_two_mod"])
 def test_mixer_taps_match_oracle(case, prec):
     z, meta, cfg, sd = load_case(case)
@@ -73,7 +74,7 @@ def test_mixer_taps_match_oracle(case, prec):
         assert rel_err(got_c.numpy(), ref_c.numpy()) <= 10 * TOL[prec]
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 def test_taps_at_config_c_shape(prec):
     """Production shape (S = 2298, N = 1838, T = 36) of each layer tap against the oracle evaluated
     in fp32 on the same GPU (random O(1) state, layer 0 weights of the config-C model)."""
@@ -97,4 +98,4 @@ def test_taps_at_config_c_shape(prec):
         ]:
             err = rel_err(got.cpu().numpy(), ref.cpu().numpy())
             print(f"{name} prec {prec}: rel err {err:.2e}")
-            assert err <= (1e-4 if prec == 0 else TOL[1]), (name, err)
+            assert err <= (TOL[1] if prec == 1 else 1e-4), (name, err)
