@@ -31,6 +31,9 @@ from multimodalpfn_amd.preprocessing import fit_preprocessing
 from multimodalpfn_amd.utils import infer_random_state
 
 
+_TRANSFORM_THREADS = 4
+
+
 def _precision(model, device: torch.device, autocast: bool, forced: torch.dtype | None) -> int:
     if forced is not None:
         return _lib.f32_precision() if forced in (torch.float32, torch.float64) else _lib.PREC_BF16
@@ -116,12 +119,24 @@ class InferenceEngine:
                 cache.clear()
                 cache["_tag"] = tag
         tokens = _mixer_tokens(model, eng, image_train, image_test, prec, cache) if mine else None
+        # the members' host transforms run on a small thread pool (numpy / sklearn release the GIL for the
+        # heavy parts), so the first unit's inputs are ready after about one transform, not one per member
+        pending = {}
+        pool = None
+        todo = [i for i in mine if members[i].X_train is not None]
+        if len(todo) > 1:
+            from concurrent.futures import ThreadPoolExecutor
+
+            pool = ThreadPoolExecutor(max_workers=min(len(todo), _TRANSFORM_THREADS))
+            pending = {i: pool.submit(lambda p=members[i].preprocessor: p.transform(X).X) for i in todo}
+
         def items():  # a generator: forward_many launches each unit as soon as its members are ready
             for i in mine:
                 m = members[i]
                 x_full = None
                 if m.X_train is not None:
-                    X_test = _h2d(m.preprocessor.transform(X).X, eng.device)
+                    xt = pending[i].result() if i in pending else m.preprocessor.transform(X).X
+                    X_test = _h2d(xt, eng.device)
                     key = ("X_train", i, str(eng.device))
                     xtr = None if cache is None else cache.get(key)
                     if xtr is None:
@@ -131,7 +146,11 @@ class InferenceEngine:
                     x_full = torch.cat([xtr, X_test], 0)
                 yield x_full, tokens, np.asarray(m.y_train, np.float32)
 
-        outs: dict[int, torch.Tensor] = dict(zip(mine, eng.forward_many(items(), prec)))
+        try:
+            outs: dict[int, torch.Tensor] = dict(zip(mine, eng.forward_many(items(), prec)))
+        finally:
+            if pool is not None:
+                pool.shutdown(wait=True)
         if mine:
             eng.status()  # NaN / HIP errors of every queued member (transformer.py:727-731,790-796)
         Q = len(X) if X is not None else len(image_test)

@@ -2,6 +2,7 @@
 # Build the whole engine with extra compile flags into multimodalpfn_amd/libmmpfn_var_<name>.so
 # (local, CPU):  tools/build_variant.sh name "-DFLAG=1 ..."
 set -o pipefail
+mkdir -p ${VAR_DIR:-multimodalpfn_amd}
 name=$1; flags=$2
 C=multimodalpfn_amd/csrc
 B=/tmp/mmpfn_var_$name
@@ -14,4 +15,4 @@ done
 wait
 printf 'const char *const mmpfn_variant_flags = "%s";\n' "$name: $flags" > $B/variant_marker.c
 gcc -fPIC -c $B/variant_marker.c -o $B/variant_marker.o || exit 1
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o multimodalpfn_amd/libmmpfn_var_$name.so $B/*.o && echo built $name
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ${VAR_DIR:-multimodalpfn_amd}/libmmpfn_var_$name.so $B/*.o && echo built $name

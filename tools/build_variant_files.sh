@@ -2,6 +2,7 @@
 # Variant library with extra flags on SOME sources only (the rest from the in-tree build/ objects):
 #   tools/build_variant_files.sh name "flags" file.hip [file.hip ...]
 set -o pipefail
+mkdir -p ${VAR_DIR:-multimodalpfn_amd}
 name=$1; flags=$2; shift 2
 C=multimodalpfn_amd/csrc; B=/tmp/mmpfn_varf_$name
 make -C $C -s >/dev/null || exit 1
@@ -13,4 +14,4 @@ for src in "$@"; do
 done
 printf 'const char *const mmpfn_variant_flags = "%s";\n' "$name: $flags" > $B/variant_marker.c
 gcc -fPIC -c $B/variant_marker.c -o $B/variant_marker.o || exit 1
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o multimodalpfn_amd/libmmpfn_var_$name.so $B/*.o && echo built $name
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ${VAR_DIR:-multimodalpfn_amd}/libmmpfn_var_$name.so $B/*.o && echo built $name
