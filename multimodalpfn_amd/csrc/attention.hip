@@ -366,11 +366,7 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
 //        inside every 16-key group stored in the order 0-3, 8-11, 4-7, 12-15 so that the
 //        keys one lane owns in the S^T accumulator (4hh + {0-3, 8-11}) are one 16-B chunk.
 constexpr int A2_KT = 64;
-#ifndef A2_NWAVES
-#define A2_NWAVES 4  // waves per block: 4 (two blocks per CU) or 8 (one 512-query block per CU, each K / V^T
-                     // chunk staged by one thread: waves 0-3 stage K, 4-7 V^T)
-#endif
-constexpr int A2_NW = A2_NWAVES;
+constexpr int A2_NW = 4;  // 8-wave (512-query) blocks measured slower: 363-372 vs 343 us at C, 1374 vs 1290 at E
 #ifndef A2_NCH
 #define A2_NCH 2  // 32-query MFMA chains per wave
 #endif
@@ -450,7 +446,7 @@ __device__ unsigned long long a2_stamp_buf[16384 * 6];
 #define A2_STAMP(i)
 #endif
 template <bool F8>
-__global__ __launch_bounds__(64 * A2_NW, A2_OCC) void attn_item2_kernel(const Attn2Args p) {
+__global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args p) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * A2_SPT][2 * 4096];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar task / activity tests
@@ -515,19 +511,14 @@ __global__ __launch_bounds__(64 * A2_NW, A2_OCC) void attn_item2_kernel(const At
   const bool partial = (p.nk % A2_KT) != 0;
 
   // ---- staging: one 16-B K chunk and one 16-B V^T chunk per thread and tile
-  const int sti = A2_NW == 8 ? (tid & 255) : tid;
-  const bool doK = A2_NW == 4 || wave < 4, doV = A2_NW == 4 || wave >= 4;  // wave-uniform
-  const int krow = sti >> 2, kc = sti & 3;      // K tile [64][32]: row, chunk
-  const int vd = sti >> 3, vc = sti & 7;        // V^T tile [32][64]: row d, natural 8-key chunk
-#if A2_NWAVES == 8 && defined(A2_YPRIO)
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (MI355X_MICROARCH item 4)
-#endif
+  const int krow = tid >> 2, kc = tid & 3;      // K tile [64][32]: row, chunk
+  const int vd = tid >> 3, vc = tid & 7;        // V^T tile [32][64]: row d, natural 8-key chunk
   u32x4 rk[A2_SPT * A2_AHEAD], rv[A2_SPT * A2_AHEAD];
   auto gload = [&](int u, int t) {  // tile t into staging registers u
     const int k0 = t * A2_KT;
-    if (doK) rk[u] = *(const u32x4*)(Kg + (int64_t)(k0 + krow) * 32 + kc * 8);
-    if (doV) rv[u] = *(const u32x4*)(Vg + (int64_t)vd * p.Npad + k0 + vc * 8);
-    if (doV && partial && t == ntiles - 1) {  // keys >= nk: V = 0 so that p = 0 never meets NaN / inf padding
+    rk[u] = *(const u32x4*)(Kg + (int64_t)(k0 + krow) * 32 + kc * 8);
+    rv[u] = *(const u32x4*)(Vg + (int64_t)vd * p.Npad + k0 + vc * 8);
+    if (partial && t == ntiles - 1) {  // keys >= nk: V = 0 so that p = 0 never meets NaN / inf padding
       bf16x8 e = __builtin_bit_cast(bf16x8, rv[u]);
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -543,8 +534,7 @@ __global__ __launch_bounds__(64 * A2_NW, A2_OCC) void attn_item2_kernel(const At
   const int f8_off1 = vd * 64 + 16 * ((2 + f8_u) ^ ((vd >> 2) & 3)) + 4 * f8_q;   // k = 32 + 16u + 4q
   auto lstore = [&](int u, int buf) {
     unsigned char* Ks = lds[buf];
-    if (doK) *(u32x4*)(Ks + koff_w) = rk[u];
-    if (!doV) return;
+    *(u32x4*)(Ks + koff_w) = rk[u];
     if constexpr (F8) {
       const bf16x8 e = __builtin_bit_cast(bf16x8, rv[u]);
       int w0 = __builtin_amdgcn_cvt_pk_fp8_f32((float)e[0], (float)e[1], 0, false);
@@ -966,7 +956,7 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
   const int krow = tid >> 2, kc = tid & 3;
   const int vd = tid >> 3, vc = tid & 7;
   f32x4 rk[2], rv[2];
-  auto gload = [&](int t) {
+  auto gload = [&](int t) __attribute__((always_inline)) {
     const int k0 = t * A2_KT;
     const float* ks = Kg + (int64_t)(k0 + krow) * 32 + kc * 8;
     const float* vs = Vg + (int64_t)vd * p.Npad + k0 + vc * 8;
@@ -980,7 +970,7 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
   };
   const int koff_w = a2_koff(krow, kc);
   const int voff_w0 = a2_voff(vd, vc & ~1) + 8 * (vc & 1), voff_w1 = a2_voff(vd, vc | 1) + 8 * (vc & 1);
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf) __attribute__((always_inline)) {
     unsigned char* Ks = lds[buf];
     bf16x8 hi, lo;
     a3_split8(rk[0], rk[1], 1.0f, hi, lo);
@@ -1019,7 +1009,7 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
     mref[qb] = 0.f;
   }
 
-  auto tile = [&](int it, auto maskc, auto firstc, auto refc) {
+  auto tile = [&](int it, auto maskc, auto firstc, auto refc) __attribute__((always_inline)) {
     constexpr bool MASK = decltype(maskc)::value;
     constexpr bool FIRST = decltype(firstc)::value;
     constexpr bool REF = decltype(refc)::value;
@@ -1107,7 +1097,7 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
   __syncthreads();
   using Y = std::true_type;
   using N = std::false_type;
-  auto pass = [&](auto wmc) {
+  auto pass = [&](auto wmc) __attribute__((always_inline)) {
     constexpr bool WM = decltype(wmc)::value;
     using F = std::integral_constant<bool, WM>;
     if (ntiles == 1) {
@@ -1120,7 +1110,7 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
       if (partial) tile(nfull, Y{}, N{}, F{});
     }
   };
-  auto rowsum = [&](int qb) {
+  auto rowsum = [&](int qb) __attribute__((always_inline)) {
     const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(lacc[qb][0]), __float_as_uint(lacc[qb][1]),
                                                     false, false);
     const auto s2 = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);
@@ -1209,9 +1199,9 @@ hipError_t launch_item_attention(const void* q, const void* k, const void* vt, v
     return hipGetLastError();
   }
 #ifdef MMPFN_ATTN_FP8PV
-  hipLaunchKernelGGL(attn_item2_kernel<true>, dim3(a.nblocks), dim3(64 * A2_NW), 0, st, a);
+  hipLaunchKernelGGL(attn_item2_kernel<true>, dim3(a.nblocks), dim3(256), 0, st, a);
 #else
-  hipLaunchKernelGGL(attn_item2_kernel<false>, dim3(a.nblocks), dim3(64 * A2_NW), 0, st, a);
+  hipLaunchKernelGGL(attn_item2_kernel<false>, dim3(a.nblocks), dim3(256), 0, st, a);
 #endif
   return hipGetLastError();
 }
