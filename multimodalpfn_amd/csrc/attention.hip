@@ -50,8 +50,20 @@ struct IaLds {
 //           sum_k p into every register of lacc, moving the adds off the VALU.
 constexpr float IA_TAU = 8.0f;
 
-template <bool BF16, int NW>
+// hi = bf16(x), lo = bf16(x - hi) of 8 fp32 values (the parity mode's split operands)
+__device__ __forceinline__ void split8v(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    hi[i] = (bf16)a[i], hi[4 + i] = (bf16)b[i];
+    lo[i] = (bf16)(a[i] - (float)hi[i]), lo[4 + i] = (bf16)(b[i] - (float)hi[4 + i]);
+  }
+}
+
+// MODE 0: fp32-input MFMA (PREC_F32_MFMA), 1: bf16, 2: parity mode on fp32 data with split-bf16 operands
+// (three products per contraction, like attn_item3); modes 0 and 2 share the fp32 LDS images
+template <int MODE, int NW>
 __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
+  constexpr bool BF16 = MODE == 1, X3 = MODE == 2;
   typedef typename std::conditional<BF16, bf16, float>::type TE;
   constexpr int EB = sizeof(TE);
   using L = IaLds<BF16>;
@@ -86,9 +98,18 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
   const int64_t qs = s0 + min(qi, nq - 1);
 
   // ---- Q fragments (B operand of S^T = K Q^T), pre-scaled by c
-  bf16x8 qb[2];
+  bf16x8 qb[2], ql[2];
   float qf[16];
-  if constexpr (BF16) {
+  if constexpr (X3) {
+    const float* qrow = (const float*)Q + qs * 32;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f32x4 a = *(const f32x4*)(qrow + 16 * ks + 8 * hh), b = *(const f32x4*)(qrow + 16 * ks + 8 * hh + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] *= c, b[i] *= c;
+      split8v(a, b, qb[ks], ql[ks]);
+    }
+  } else if constexpr (BF16) {
     const bf16* qrow = (const bf16*)Q + qs * 32;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -188,7 +209,23 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
 
     // ---- S^T - m_ref for the two 32-key subtiles
     f32x16 sacc[2];
-    if constexpr (BF16) {
+    if constexpr (X3) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const unsigned char* krow = Ks + (32 * u + r) * L::KROW;
+        bf16x8 kh[2], kl[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          split8v(*(const f32x4*)(krow + (16 * ks + 8 * hh) * 4), *(const f32x4*)(krow + (16 * ks + 8 * hh + 4) * 4),
+                  kh[ks], kl[ks]);
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[0], qb[0], negm, 0, 0, 0);
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[1], qb[1], sacc[u], 0, 0, 0);
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[0], ql[0], sacc[u], 0, 0, 0);
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[1], ql[1], sacc[u], 0, 0, 0);
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[0], qb[0], sacc[u], 0, 0, 0);
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[1], qb[1], sacc[u], 0, 0, 0);
+      }
+    } else if constexpr (BF16) {
       // all four K fragments in flight before the first MFMA (the scheduler otherwise
       // serialises read -> wait -> MFMA and exposes the LDS latency four times)
       bf16x8 kf[2][2];
@@ -208,7 +245,7 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const unsigned char* krow = Ks + (32 * u + r) * L::KROW;
-      if constexpr (BF16) {
+      if constexpr (BF16 || X3) {
       } else {
         float kf[16];
 #pragma unroll
@@ -261,7 +298,25 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const unsigned char* vrow = Vs + r * L::VROW;
-      if constexpr (BF16) {
+      if constexpr (X3) {
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          f32x4 pa, pc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pa[j] = exp2f(sacc[u][8 * sp + j]);
+            pc[j] = exp2f(sacc[u][8 * sp + 4 + j]);
+            lsum += pa[j] + pc[j];
+          }
+          bf16x8 ph, pl, vh, vl;
+          split8v(pa, pc, ph, pl);
+          const int kb = 32 * u + 16 * sp + 4 * hh;
+          split8v(*(const f32x4*)(vrow + kb * 4), *(const f32x4*)(vrow + (kb + 8) * 4), vh, vl);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph, o, 0, 0, 0);
+        }
+      } else if constexpr (BF16) {
 #pragma unroll
         for (int sp = 0; sp < 2; ++sp) {
           bf16x8 pb;
@@ -1226,11 +1281,14 @@ hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int nw, hipStre
   if (nw != 1 && nw != 4) return hipErrorInvalidValue;
   dim3 grid((a.nq + 32 * nw - 1) / (32 * nw), a.H, batches);
   if (prec == PREC_BF16) {
-    if (nw == 4) hipLaunchKernelGGL((attn_item_kernel<true, 4>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((attn_item_kernel<true, 1>), grid, dim3(64), 0, st, a);
+    if (nw == 4) hipLaunchKernelGGL((attn_item_kernel<1, 4>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_item_kernel<1, 1>), grid, dim3(64), 0, st, a);
+  } else if (prec == PREC_F32) {  // parity mode: split-bf16 products (the feature attention's path)
+    if (nw == 4) hipLaunchKernelGGL((attn_item_kernel<2, 4>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_item_kernel<2, 1>), grid, dim3(64), 0, st, a);
   } else {
-    if (nw == 4) hipLaunchKernelGGL((attn_item_kernel<false, 4>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((attn_item_kernel<false, 1>), grid, dim3(64), 0, st, a);
+    if (nw == 4) hipLaunchKernelGGL((attn_item_kernel<0, 4>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_item_kernel<0, 1>), grid, dim3(64), 0, st, a);
   }
   return hipGetLastError();
 }

@@ -537,8 +537,7 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
     RC(ensure(ctx, ctx->ws_X, (size_t)M * R * E * 4));
     RC(ensure(ctx, ctx->ws_O, (size_t)M * R * E * 4));
     const size_t Tpad = (T + 63) / 64 * 64;
-    size_t big = std::max(R * E + (size_t)2 * S * Tpad * E, (size_t)M * (R * E + (size_t)2 * T * Npad * E)) * 4;
-    if (prec == PREC_F32) big = std::max(big, (size_t)M * R * d.nhid * 4);  // the parity-mode MLP's hidden rows
+    const size_t big = std::max(R * E + (size_t)2 * S * Tpad * E, (size_t)M * (R * E + (size_t)2 * T * Npad * E)) * 4;
     RC(ensure(ctx, ctx->ws_big, big));
     RC(ensure(ctx, ctx->ws_pe, (size_t)(G + C + 1) * E * 4));
     RC(ensure(ctx, ctx->ws_slots, (size_t)(G + 1) * fpg * sizeof(SlotParams)));
@@ -763,21 +762,10 @@ int mlp_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int64_t RM, int p
   if (mlp_fuses_out(d, prec)) {  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders
     HIPCHK(launch_mlp_rows(Xall, L.mlp1_h.p, L.mlp2_h.p, RM, d.emsize, d.nhid, d.ln_eps, ctx->stream, O,
                            O ? L.item_out_h.p : nullptr));
-  } else if (prec == PREC_F32) {
-    // parity mode: up-projection + GELU(erf) and down-projection + residual + LN as two split-bf16 GEMMs,
-    // the hidden rows [RM][nhid] fp32 in the (by now free) attention scratch
-    RC(ensure(ctx, ctx->ws_big, (size_t)RM * d.nhid * 4));
-    float* Hd = (float*)ctx->ws_big.p;
-    GemmArgs u = gargs();
-    u.A = Xall, u.lda = d.emsize, u.act = ACT_GELU;
-    setw(ctx, u, L.mlp1, L.mlp1_h, prec);
-    u.M = (int)RM, u.N = d.nhid, u.K = d.emsize, u.C = Hd, u.ldc = d.nhid;
-    HIPCHK(launch_gemm(u, prec, EPI_STORE, true, true, 1, ctx->stream));
-    GemmArgs dn = gargs();
-    dn.A = Hd, dn.lda = d.nhid;
-    setw(ctx, dn, L.mlp2, L.mlp2_h, prec);
-    dn.M = (int)RM, dn.N = d.emsize, dn.K = d.nhid, dn.X = Xall, dn.ln_eps = d.ln_eps;
-    HIPCHK(launch_gemm(dn, prec, EPI_RES_LN, true, true, 1, ctx->stream));
+  } else if (prec == PREC_F32) {  // parity mode: the fused MLP on split-bf16 products (W1 / W2 hi | lo planes)
+    const auto w1 = ctx->split.find(L.mlp1.p), w2 = ctx->split.find(L.mlp2.p);
+    if (w1 == ctx->split.end() || w2 == ctx->split.end()) return fail(ctx, MMPFN_ERR_STATE, "no split MLP weights");
+    HIPCHK(launch_mlp_fused(Xall, w1->second.p, w2->second.p, RM, d.emsize, d.nhid, d.ln_eps, PREC_F32, ctx->stream));
   } else {
     HIPCHK(launch_mlp_fused(Xall, L.mlp1.p, L.mlp2.p, RM, d.emsize, d.nhid, d.ln_eps, PREC_F32_MFMA, ctx->stream));
   }

@@ -21,21 +21,28 @@ constexpr int ME = 192;   // model width
 constexpr int MWROW = 144;  // LDS bytes per staged W row (128 + 16 pad)
 constexpr int MLN_STRIDE = 196;
 
-template <bool BF16>
+// MODE 0: fp32-input MFMA (PREC_F32_MFMA), 1: bf16, 2: parity mode (PREC_F32): X and the GELU'd hidden
+// chunk split into bf16 hi / lo planes in LDS, W1 / W2 given as hi | lo planes (capi.cpp upsplit), three
+// bf16 products per contraction; 157 KB of LDS, one block per CU
+template <int MODE>
 struct MlpLds {
-  static constexpr int EB = BF16 ? 2 : 4;
+  static constexpr int NP = MODE == 2 ? 2 : 1;  // operand planes
+  static constexpr int EB = MODE == 0 ? 4 : 2;
   static constexpr int AROW = ME * EB + 16;  // bytes per A / H row
   static constexpr int A_BYTES = MBM * AROW;
   static constexpr int W_BYTES = ME * MWROW;
-  static constexpr int TOTAL = 2 * A_BYTES + W_BYTES;
+  static constexpr int TOTAL = NP * (2 * A_BYTES + W_BYTES);
   static constexpr int LN_BYTES = MBM * MLN_STRIDE * 4;
   static constexpr int BYTES = TOTAL > LN_BYTES ? TOTAL : LN_BYTES;
 };
 
-template <bool BF16>
-__global__ __launch_bounds__(256, 2) void mlp_fused_kernel(float* __restrict__ X, const void* __restrict__ W1p,
-                                                          const void* __restrict__ W2p, int M, int Fh, float eps) {
-  using L = MlpLds<BF16>;
+template <int MODE>
+__global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float* __restrict__ X,
+                                                                           const void* __restrict__ W1p,
+                                                                           const void* __restrict__ W2p, int M, int Fh,
+                                                                           float eps) {
+  constexpr bool BF16 = MODE != 0, X3 = MODE == 2;
+  using L = MlpLds<MODE>;
   constexpr int EB = L::EB;
   constexpr int BK = 128 / EB;          // K per W slice
   constexpr int SPC = ME / BK;          // slices per 192-wide contraction (3 bf16 / 6 f32)
@@ -43,8 +50,12 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_kernel(float* __restrict__ X
   unsigned char* As = smem;
   unsigned char* Hs = smem + L::A_BYTES;
   unsigned char* Ws = smem + 2 * L::A_BYTES;
+  unsigned char* Asl = smem + 2 * L::A_BYTES + L::W_BYTES;  // x3 lo planes
+  unsigned char* Hsl = Asl + L::A_BYTES;
+  unsigned char* Wsl = Hsl + L::A_BYTES;
   const unsigned char* W1 = (const unsigned char*)W1p;
   const unsigned char* W2 = (const unsigned char*)W2p;
+  const int64_t lo1 = X3 ? (int64_t)Fh * ME * 2 : 0, lo2 = lo1;  // bytes from a hi plane to its lo plane
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -58,7 +69,13 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_kernel(float* __restrict__ X
     const int64_t m = m0 + row;
     f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
     if (m < M) v = *(const f32x4*)(X + m * ME + c4 * 4);
-    if constexpr (BF16) {
+    if constexpr (X3) {
+      bf16x4 b, l;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[i] = (bf16)v[i], l[i] = (bf16)(v[i] - (float)b[i]);
+      *(bf16x4*)(As + row * L::AROW + c4 * 8) = b;
+      *(bf16x4*)(Asl + row * L::AROW + c4 * 8) = l;
+    } else if constexpr (BF16) {
       bf16x4 b;
       b[0] = (bf16)v[0]; b[1] = (bf16)v[1]; b[2] = (bf16)v[2]; b[3] = (bf16)v[3];
       *(bf16x4*)(As + row * L::AROW + c4 * 8) = b;
@@ -69,12 +86,13 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_kernel(float* __restrict__ X
 
   // ---- W slice staging (16-byte chunks, 6 per thread); a slice is 192 rows x 128 B
   constexpr int WCH = ME * 8 / 256;
-  u32x4 rw[WCH];
+  u32x4 rw[WCH], rwl[X3 ? WCH : 1];
   auto wload = [&](const unsigned char* base, int64_t ld_bytes) {
 #pragma unroll
     for (int j = 0; j < WCH; ++j) {
       const int cidx = tid + 256 * j;
       rw[j] = *(const u32x4*)(base + (cidx >> 3) * ld_bytes + (cidx & 7) * 16);
+      if constexpr (X3) rwl[j] = *(const u32x4*)(base + lo1 + (cidx >> 3) * ld_bytes + (cidx & 7) * 16);
     }
   };
   // W1 [Fh][E]: slice (c, ks) = rows c*192.., cols ks*BK..;  W2 [E][Fh]: rows 0..191, cols c*192 + ks*BK..
@@ -85,8 +103,10 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_kernel(float* __restrict__ X
     for (int j = 0; j < WCH; ++j) {
       const int cidx = tid + 256 * j;
       *(u32x4*)(Ws + (cidx >> 3) * MWROW + (cidx & 7) * 16) = rw[j];
+      if constexpr (X3) *(u32x4*)(Wsl + (cidx >> 3) * MWROW + (cidx & 7) * 16) = rwl[j];
     }
   };
+  (void)lo2;
 
   f32x4 accy[2][6], acch[2][6];
 #pragma unroll
@@ -98,7 +118,28 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_kernel(float* __restrict__ X
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int kb = ks * 128 + kk * 64 + fg * 16;  // byte offset inside the A/H row
-      if constexpr (BF16) {
+      if constexpr (X3) {
+        const unsigned char* Asl_ = Asrc == As ? Asl : Hsl;
+        bf16x8 af[2], afl[2], bw[6], bwl[6];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          af[mt] = *(const bf16x8*)(Asrc + (wm * 32 + mt * 16 + fr) * L::AROW + kb);
+          afl[mt] = *(const bf16x8*)(Asl_ + (wm * 32 + mt * 16 + fr) * L::AROW + kb);
+        }
+#pragma unroll
+        for (int nt = 0; nt < 6; ++nt) {
+          bw[nt] = *(const bf16x8*)(Ws + (wn * 96 + nt * 16 + fr) * MWROW + kk * 64 + fg * 16);
+          bwl[nt] = *(const bf16x8*)(Wsl + (wn * 96 + nt * 16 + fr) * MWROW + kk * 64 + fg * 16);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 6; ++nt) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[mt], bw[nt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bwl[nt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bw[nt], acc[mt][nt], 0, 0, 0);
+          }
+      } else if constexpr (BF16) {
         bf16x8 af[2], bw[6];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) af[mt] = *(const bf16x8*)(Asrc + (wm * 32 + mt * 16 + fr) * L::AROW + kb);
@@ -148,7 +189,12 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_kernel(float* __restrict__ X
         for (int r = 0; r < 4; ++r) {
           const int rl = wm * 32 + mt * 16 + fg * 4 + r;
           const int cl = wn * 96 + nt * 16 + fr;
-          if constexpr (BF16)
+          if constexpr (X3) {
+            const float g = gelu_erf(acch[mt][nt][r]);
+            const bf16 gh = (bf16)g;
+            *(bf16*)(Hs + rl * L::AROW + cl * 2) = gh;
+            *(bf16*)(Hsl + rl * L::AROW + cl * 2) = (bf16)(g - (float)gh);
+          } else if constexpr (BF16)
             *(bf16*)(Hs + rl * L::AROW + cl * 2) = (bf16)gelu_tanh_fast(acch[mt][nt][r]);
           else
             *(float*)(Hs + rl * L::AROW + cl * 4) = gelu_erf(acch[mt][nt][r]);
@@ -225,19 +271,23 @@ hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M,
   dim3 grid((M + MBM - 1) / MBM);
   static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)mlp_fused_kernel<true>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, MlpLds<true>::BYTES);
+    hipError_t e = hipFuncSetAttribute((const void*)mlp_fused_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       MlpLds<1>::BYTES);
     if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)mlp_fused_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            MlpLds<false>::BYTES);
+    e = hipFuncSetAttribute((const void*)mlp_fused_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            MlpLds<0>::BYTES);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void*)mlp_fused_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            MlpLds<2>::BYTES);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   if (prec == PREC_BF16)
-    hipLaunchKernelGGL(mlp_fused_kernel<true>, grid, dim3(256), MlpLds<true>::BYTES, st, X, W1, W2, (int)M, Fh, eps);
+    hipLaunchKernelGGL(mlp_fused_kernel<1>, grid, dim3(256), MlpLds<1>::BYTES, st, X, W1, W2, (int)M, Fh, eps);
+  else if (prec == PREC_F32)  // W1 / W2: hi | lo planes
+    hipLaunchKernelGGL(mlp_fused_kernel<2>, grid, dim3(256), MlpLds<2>::BYTES, st, X, W1, W2, (int)M, Fh, eps);
   else
-    hipLaunchKernelGGL(mlp_fused_kernel<false>, grid, dim3(256), MlpLds<false>::BYTES, st, X, W1, W2, (int)M, Fh,
-                       eps);
+    hipLaunchKernelGGL(mlp_fused_kernel<0>, grid, dim3(256), MlpLds<0>::BYTES, st, X, W1, W2, (int)M, Fh, eps);
   return hipGetLastError();
 }
 
