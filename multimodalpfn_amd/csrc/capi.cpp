@@ -35,7 +35,6 @@ struct LayerW {  // packed per layer, [N][K] row-major
   DevBuf feat_qkv, feat_out, item_qkv, item_qtest, item_out, mlp1, mlp2;  // fp32
   DevBuf feat_qkv_h, feat_out_h, item_qkv_h, item_qtest_h, item_out_h, mlp1_h, mlp2_h;  // bf16
   DevBuf feat_pack_h;  // bf16 LDS images of the feature-attention weights (featrow.hip)
-  DevBuf mlp1_q, mlp2_q;  // bf16 W1 / W2 in mlp32_kernel's K orders (mlp32.hip)
 };
 
 uint16_t f2bf(float f) {  // round-to-nearest-even, NaN preserving
@@ -223,32 +222,6 @@ std::vector<float> pack_mlp1_perm(const std::vector<float>& w, int E, int Fh) {
   return o;
 }
 
-// W1 [Fh][E] in mlp32_kernel's af K order: position 16ks + 8hh + m holds feature
-// 32(ks>>1) + 16(ks&1) + (m&3) + 8(m>>2) + 4hh (the Y^T accumulator layout of a 32x32 tile)
-std::vector<float> pack_mlp1_perm32(const std::vector<float>& w, int E, int Fh) {
-  std::vector<float> o(w.size());
-  for (int h = 0; h < Fh; ++h)
-    for (int p = 0; p < E; ++p) {
-      const int ks = p / 16, hh = (p % 16) / 8, m = p % 8;
-      const int f = 32 * (ks >> 1) + 16 * (ks & 1) + (m & 3) + 8 * (m >> 2) + 4 * hh;
-      o[(size_t)h * E + p] = w[(size_t)h * E + f];
-    }
-  return o;
-}
-
-// W2 [E][Fh] with each 32-hidden chunk in mlp32_kernel's H^T order: position 16j + 8hh + m holds
-// hidden 16j + (m&3) + 8(m>>2) + 4hh of the chunk (the 32x32 accumulator rows of a lane)
-std::vector<float> pack_mlp2_perm32(const std::vector<float>& w, int E, int Fh) {
-  std::vector<float> o(w.size());
-  for (int e = 0; e < E; ++e)
-    for (int c = 0; c < Fh; c += 32)
-      for (int q = 0; q < 32; ++q) {
-        const int j = q / 16, hh = (q % 16) / 8, m = q % 8;
-        o[(size_t)e * Fh + c + q] = w[(size_t)e * Fh + c + 16 * j + (m & 3) + 8 * (m >> 2) + 4 * hh];
-      }
-  return o;
-}
-
 // featrow.hip weight pack (FEAT_PACK_LAYER floats, LDS images with FEAT_IMG_STRIDE-wide rows,
 // the 16 pad columns zero):
 //   per head h, rows [0,32) : Wq row 8(rho>>2) + 4f + (rho&3) for image row 16f + rho, scaled by
@@ -346,10 +319,6 @@ int finalize(mmpfn_ctx* ctx) {
     if ((rc = upload(ctx, L.mlp2, *m2, false))) return rc;
     if ((rc = upsplit(ctx, L.mlp2, *m2))) return rc;
     if ((rc = upload(ctx, L.mlp2_h, pack_mlp2_perm(*m2, E, Fh), true))) return rc;
-    if (E == 192) {
-      if ((rc = upload(ctx, L.mlp1_q, pack_mlp1_perm32(*m1, E, Fh), true))) return rc;
-      if ((rc = upload(ctx, L.mlp2_q, pack_mlp2_perm32(*m2, E, Fh), true))) return rc;
-    }
     std::vector<float> wtrain((size_t)3 * HD * E), wtest((size_t)HD * E);
     if (d.two_sets_of_queries) {
       GETW(wq, p + "self_attn_between_items._w_q", (size_t)2 * HD * E);
@@ -791,14 +760,7 @@ bool mlp_fuses_out(const mmpfn_model_desc& d, int prec) { return prec == PREC_BF
 // ---- MLP (mlp.py:93-104) + residual + LN over RM tokens; O non-null: the fused out-projection first
 int mlp_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int64_t RM, int prec, const void* O) {
   const mmpfn_model_desc& d = ctx->d;
-  static const bool mlp32 = [] {
-    const char* e = getenv("MMPFN_MLP32");
-    return e && e[0] == '1';
-  }();
-  if (mlp_fuses_out(d, prec) && mlp32) {  // 32x32x16 MFMA variant (mlp32.hip), W1 / W2 in its K orders
-    HIPCHK(launch_mlp32(Xall, L.mlp1_q.p, L.mlp2_q.p, RM, d.emsize, d.nhid, d.ln_eps, ctx->stream, O,
-                        O ? L.item_out_h.p : nullptr));
-  } else if (mlp_fuses_out(d, prec)) {  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders
+  if (mlp_fuses_out(d, prec)) {  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders
     HIPCHK(launch_mlp_rows(Xall, L.mlp1_h.p, L.mlp2_h.p, RM, d.emsize, d.nhid, d.ln_eps, ctx->stream, O,
                            O ? L.item_out_h.p : nullptr));
   } else if (prec == PREC_F32) {  // parity mode: the fused MLP on split-bf16 products (W1 / W2 hi | lo planes)
@@ -997,7 +959,7 @@ void mmpfn_destroy(mmpfn_ctx* ctx) {
   for (auto& L : ctx->layers) {
     for (DevBuf* b : {&L.feat_qkv, &L.feat_out, &L.item_qkv, &L.item_qtest, &L.item_out, &L.mlp1, &L.mlp2,
                       &L.feat_qkv_h, &L.feat_out_h, &L.item_qkv_h, &L.item_qtest_h, &L.item_out_h, &L.mlp1_h,
-                      &L.mlp2_h, &L.feat_pack_h, &L.mlp1_q, &L.mlp2_q})
+                      &L.mlp2_h, &L.feat_pack_h})
       fr(*b);
   }
   for (DevBuf* b : {&ctx->enc_w, &ctx->y_w, &ctx->y_b, &ctx->pe_w, &ctx->pe_b, &ctx->dec_w1, &ctx->dec_b1,

@@ -68,9 +68,6 @@ hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M,
 // permuted hidden order of pack_mlp2_perm (capi.cpp); Fh % 32 == 0, E == 192
 // W1perm: W1 with its K (feature) order permuted to the Y^T lane layout (capi.cpp pack_mlp1_perm);
 // O / Wout non-null: X <- LN(X + O Wout^T) first (the item-attention out-projection, fused)
-// the same sublayer on 32x32x16 MFMAs (mlp32.hip); W1 / W2 in its K orders (capi.cpp pack_mlp*_perm32)
-hipError_t launch_mlp32(float* X, const void* W1perm, const void* W2perm, int64_t M, int E, int Fh, float eps,
-                        hipStream_t st, const void* O, const void* Wout);
 hipError_t launch_mlp_rows(float* X, const void* W1perm, const void* W2perm, int64_t M, int E, int Fh, float eps,
                            hipStream_t st, const void* O = nullptr, const void* Wout = nullptr);
 

@@ -28,13 +28,20 @@ template <int MODE>
 struct MlpLds {
   static constexpr int NP = MODE == 2 ? 2 : 1;  // operand planes
   static constexpr int EB = MODE == 0 ? 4 : 2;
-  static constexpr int AROW = ME * EB + 16;  // bytes per A / H row
+  // x3: unpadded 384-B A / H rows with 16-B units XOR-swizzled by (row >> 1) & 7 and 160-B W rows -- both
+  // conflict-free for the 16x16x32 fragment reads, and the five images fit 160 KB (2-way conflicts with
+  // the padded 400 / 144-B rows of the other modes)
+  static constexpr int AROW = MODE == 2 ? ME * EB : ME * EB + 16;  // bytes per A / H row
+  static constexpr int WROW = MODE == 2 ? 160 : MWROW;             // bytes per staged W row
   static constexpr int A_BYTES = MBM * AROW;
-  static constexpr int W_BYTES = ME * MWROW;
+  static constexpr int W_BYTES = ME * WROW;
   static constexpr int TOTAL = NP * (2 * A_BYTES + W_BYTES);
   static constexpr int LN_BYTES = MBM * MLN_STRIDE * 4;
   static constexpr int BYTES = TOTAL > LN_BYTES ? TOTAL : LN_BYTES;
 };
+
+// byte offset of byte b of row r in an x3 A / H image
+__device__ __forceinline__ int x3_aoff(int r, int b) { return r * (ME * 2) + ((((b >> 4) ^ ((r >> 1) & 7))) << 4) + (b & 15); }
 
 template <int MODE>
 __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float* __restrict__ X,
@@ -73,8 +80,8 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
       bf16x4 b, l;
 #pragma unroll
       for (int i = 0; i < 4; ++i) b[i] = (bf16)v[i], l[i] = (bf16)(v[i] - (float)b[i]);
-      *(bf16x4*)(As + row * L::AROW + c4 * 8) = b;
-      *(bf16x4*)(Asl + row * L::AROW + c4 * 8) = l;
+      *(bf16x4*)(As + x3_aoff(row, c4 * 8)) = b;
+      *(bf16x4*)(Asl + x3_aoff(row, c4 * 8)) = l;
     } else if constexpr (BF16) {
       bf16x4 b;
       b[0] = (bf16)v[0]; b[1] = (bf16)v[1]; b[2] = (bf16)v[2]; b[3] = (bf16)v[3];
@@ -102,8 +109,8 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
 #pragma unroll
     for (int j = 0; j < WCH; ++j) {
       const int cidx = tid + 256 * j;
-      *(u32x4*)(Ws + (cidx >> 3) * MWROW + (cidx & 7) * 16) = rw[j];
-      if constexpr (X3) *(u32x4*)(Wsl + (cidx >> 3) * MWROW + (cidx & 7) * 16) = rwl[j];
+      *(u32x4*)(Ws + (cidx >> 3) * L::WROW + (cidx & 7) * 16) = rw[j];
+      if constexpr (X3) *(u32x4*)(Wsl + (cidx >> 3) * L::WROW + (cidx & 7) * 16) = rwl[j];
     }
   };
   (void)lo2;
@@ -123,13 +130,13 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
         bf16x8 af[2], afl[2], bw[6], bwl[6];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-          af[mt] = *(const bf16x8*)(Asrc + (wm * 32 + mt * 16 + fr) * L::AROW + kb);
-          afl[mt] = *(const bf16x8*)(Asl_ + (wm * 32 + mt * 16 + fr) * L::AROW + kb);
+          af[mt] = *(const bf16x8*)(Asrc + x3_aoff(wm * 32 + mt * 16 + fr, kb));
+          afl[mt] = *(const bf16x8*)(Asl_ + x3_aoff(wm * 32 + mt * 16 + fr, kb));
         }
 #pragma unroll
         for (int nt = 0; nt < 6; ++nt) {
-          bw[nt] = *(const bf16x8*)(Ws + (wn * 96 + nt * 16 + fr) * MWROW + kk * 64 + fg * 16);
-          bwl[nt] = *(const bf16x8*)(Wsl + (wn * 96 + nt * 16 + fr) * MWROW + kk * 64 + fg * 16);
+          bw[nt] = *(const bf16x8*)(Ws + (wn * 96 + nt * 16 + fr) * L::WROW + kk * 64 + fg * 16);
+          bwl[nt] = *(const bf16x8*)(Wsl + (wn * 96 + nt * 16 + fr) * L::WROW + kk * 64 + fg * 16);
         }
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
@@ -192,8 +199,8 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
           if constexpr (X3) {
             const float g = gelu_erf(acch[mt][nt][r]);
             const bf16 gh = (bf16)g;
-            *(bf16*)(Hs + rl * L::AROW + cl * 2) = gh;
-            *(bf16*)(Hsl + rl * L::AROW + cl * 2) = (bf16)(g - (float)gh);
+            *(bf16*)(Hs + x3_aoff(rl, cl * 2)) = gh;
+            *(bf16*)(Hsl + x3_aoff(rl, cl * 2)) = (bf16)(g - (float)gh);
           } else if constexpr (BF16)
             *(bf16*)(Hs + rl * L::AROW + cl * 2) = (bf16)gelu_tanh_fast(acch[mt][nt][r]);
           else
