@@ -390,6 +390,119 @@ __global__ __launch_bounds__(64 * NW) void attn_item_kernel(const AttnArgs p) {
   }
 }
 
+// ------------------------------------------------------------------ feature attention, parity mode
+// PREC_F32 attention between features (layer.py:332-339): per table row s and head h, the row's T <= 64
+// tokens attend to each other.  One wave per (row, head): queries as two 32-token chains, keys as one
+// 64-key tile, every operand loaded from the fp32 Q / K / V^T layouts straight into MFMA fragment
+// registers and split into bf16 hi + lo (no LDS: a row's tile is read by one wave only).  Exact single-
+// tile softmax (row max over the T valid keys), S^T and O^T on three split products each
+// (v_mfma_f32_32x32x16_bf16), row sums in fp32 on the VALU.  Keys >= T are masked (K / V padding rows
+// are never written by the projection: V is zeroed in registers so p = 0 never meets NaN).
+__global__ __launch_bounds__(256, 2) void attn_feat3_kernel(const AttnArgs p, int nrows) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int pair = blockIdx.x * 4 + wave;  // (row, head)
+  if (pair >= nrows * p.H) return;         // wave-uniform; no barrier follows
+  const int b = pair / p.H, h = pair - b * p.H;
+  const int T = p.nk;
+  const float* Q = (const float*)p.q + b * p.q_bstride + h * p.q_hstride;
+  const float* Kg = (const float*)p.k + b * p.kv_bstride + h * p.kv_hstride;
+  const float* Vg = (const float*)p.vt + b * p.kv_bstride + h * p.kv_hstride;
+  const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
+
+  // K (A operand of S^T = K Q^T): lane row 32u + r, dims 16ks + 8hh .. +7; V^T (A operand of O^T = V^T P^T):
+  // lane dim r, keys kb .. kb+3, kb+8 .. kb+11 with kb = 32u + 16sp + 4hh (the P^T register order)
+  bf16x8 kh[2][2], kl[2][2], vh[2][2], vl[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int key = 32 * u + r;
+    const float* kr = Kg + (int64_t)min(key, T - 1) * 32;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      split8v(*(const f32x4*)(kr + 16 * ks + 8 * hh), *(const f32x4*)(kr + 16 * ks + 8 * hh + 4), kh[u][ks], kl[u][ks]);
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {
+      const int kb = 32 * u + 16 * sp + 4 * hh;
+      const float* vr = Vg + (int64_t)r * p.kpad;
+      f32x4 a = kb < T ? *(const f32x4*)(vr + kb) : f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 e = kb + 8 < T ? *(const f32x4*)(vr + kb + 8) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (kb + j >= T) a[j] = 0.f;
+        if (kb + 8 + j >= T) e[j] = 0.f;
+      }
+      split8v(a, e, vh[u][sp], vl[u][sp]);
+    }
+  }
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {
+    const int t = 32 * ch + r;
+    if (32 * ch >= T) break;  // wave-uniform
+    bf16x8 qh[2], ql[2];
+    const float* qr = Q + (int64_t)min(t, T - 1) * 32;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f32x4 a = *(const f32x4*)(qr + 16 * ks + 8 * hh), e = *(const f32x4*)(qr + 16 * ks + 8 * hh + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] *= c, e[i] *= c;
+      split8v(a, e, qh[ks], ql[ks]);
+    }
+    f32x16 st[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const f32x16 z = {};
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[u][0], qh[0], z, 0, 0, 0);
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[u][1], qh[1], st[u], 0, 0, 0);
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[u][0], ql[0], st[u], 0, 0, 0);
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[u][1], ql[1], st[u], 0, 0, 0);
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[u][0], qh[0], st[u], 0, 0, 0);
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[u][1], qh[1], st[u], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (32 * u + (i & 3) + 8 * (i >> 2) + 4 * hh >= T) st[u][i] = -INFINITY;
+    }
+    float m = fmaxf(st[0][0], st[1][0]);
+#pragma unroll
+    for (int i = 1; i < 16; ++i) m = fmaxf(m, fmaxf(st[0][i], st[1][i]));
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+      m = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    float l = 0.f;
+    f32x16 o = {};
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        f32x4 pa, pc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pa[j] = exp2f(st[u][8 * sp + j] - m);
+          pc[j] = exp2f(st[u][8 * sp + 4 + j] - m);
+          l += pa[j] + pc[j];
+        }
+        bf16x8 ph, pl;
+        split8v(pa, pc, ph, pl);
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl[u][sp], ph, o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[u][sp], pl, o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[u][sp], ph, o, 0, 0, 0);
+      }
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+      l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    }
+    if (t < T) {
+      const float inv = 1.0f / l;
+      float* orow = (float*)p.o + (b * p.o_bstride + (int64_t)t * p.o_qstride) * (p.H * 32) + h * 32;
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq)
+        *(f32x4*)(orow + 8 * gq + 4 * hh) =
+            f32x4{o[4 * gq] * inv, o[4 * gq + 1] * inv, o[4 * gq + 2] * inv, o[4 * gq + 3] * inv};
+    }
+  }
+}
+
 // ------------------------------------------------------------------ item attention v2 (bf16)
 // Sample-axis attention of one layer in ONE launch: the train rows against their own
 // head's K/V (layer.py:362-372) and the test rows of all heads against head 0's K/V
@@ -1277,6 +1390,13 @@ hipError_t launch_attn_item3(const void* q, const void* k, const void* vt, void*
 
 hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int nw, hipStream_t st) {
   if (a.nq <= 0 || batches <= 0) return hipSuccess;
+  if (prec == PREC_F32 && nw == 1 && a.s0 == 0 && a.nq == a.nk && a.nk <= 64 && a.kvh_fixed < 0) {
+    // parity-mode feature attention: one wave per (row, head), operands straight to registers
+    if (a.kpad % 4 != 0) return hipErrorInvalidValue;
+    const int pairs = batches * a.H;
+    hipLaunchKernelGGL(attn_feat3_kernel, dim3((pairs + 3) / 4), dim3(256), 0, st, a, batches);
+    return hipGetLastError();
+  }
   if (a.nk <= 0 || a.kpad % IA_KT != 0 || a.nk > a.kpad) return hipErrorInvalidValue;
   if (nw != 1 && nw != 4) return hipErrorInvalidValue;
   dim3 grid((a.nq + 32 * nw - 1) / (32 * nw), a.H, batches);
