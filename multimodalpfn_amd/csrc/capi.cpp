@@ -319,6 +319,7 @@ int finalize(mmpfn_ctx* ctx) {
     if ((rc = upload(ctx, L.mlp2, *m2, false))) return rc;
     if ((rc = upsplit(ctx, L.mlp2, *m2))) return rc;
     if ((rc = upload(ctx, L.mlp2_h, pack_mlp2_perm(*m2, E, Fh), true))) return rc;
+    if ((rc = upsplit(ctx, L.mlp2_h, pack_mlp2_perm(*m2, E, Fh)))) return rc;  // parity mode (mlp_x3_kernel)
     std::vector<float> wtrain((size_t)3 * HD * E), wtest((size_t)HD * E);
     if (d.two_sets_of_queries) {
       GETW(wq, p + "self_attn_between_items._w_q", (size_t)2 * HD * E);
@@ -763,8 +764,8 @@ int mlp_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int64_t RM, int p
   if (mlp_fuses_out(d, prec)) {  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders
     HIPCHK(launch_mlp_rows(Xall, L.mlp1_h.p, L.mlp2_h.p, RM, d.emsize, d.nhid, d.ln_eps, ctx->stream, O,
                            O ? L.item_out_h.p : nullptr));
-  } else if (prec == PREC_F32) {  // parity mode: the fused MLP on split-bf16 products (W1 / W2 hi | lo planes)
-    const auto w1 = ctx->split.find(L.mlp1.p), w2 = ctx->split.find(L.mlp2.p);
+  } else if (prec == PREC_F32) {  // parity mode: mlp_x3_kernel on split-bf16 products (W1 / W2 hi | lo planes)
+    const auto w1 = ctx->split.find(L.mlp1.p), w2 = ctx->split.find(L.mlp2_h.p);  // W1 natural, W2 permuted
     if (w1 == ctx->split.end() || w2 == ctx->split.end()) return fail(ctx, MMPFN_ERR_STATE, "no split MLP weights");
     HIPCHK(launch_mlp_fused(Xall, w1->second.p, w2->second.p, RM, d.emsize, d.nhid, d.ln_eps, PREC_F32, ctx->stream));
   } else {

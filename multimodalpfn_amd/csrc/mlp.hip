@@ -21,34 +21,25 @@ constexpr int ME = 192;   // model width
 constexpr int MWROW = 144;  // LDS bytes per staged W row (128 + 16 pad)
 constexpr int MLN_STRIDE = 196;
 
-// MODE 0: fp32-input MFMA (PREC_F32_MFMA), 1: bf16, 2: parity mode (PREC_F32): X and the GELU'd hidden
-// chunk split into bf16 hi / lo planes in LDS, W1 / W2 given as hi | lo planes (capi.cpp upsplit), three
-// bf16 products per contraction; 157 KB of LDS, one block per CU
+// MODE 0: fp32-input MFMA (PREC_F32_MFMA), 1: bf16 (the parity mode runs mlp_x3_kernel below)
 template <int MODE>
 struct MlpLds {
-  static constexpr int NP = MODE == 2 ? 2 : 1;  // operand planes
   static constexpr int EB = MODE == 0 ? 4 : 2;
-  // x3: unpadded 384-B A / H rows with 16-B units XOR-swizzled by (row >> 1) & 7 and 160-B W rows -- both
-  // conflict-free for the 16x16x32 fragment reads, and the five images fit 160 KB (2-way conflicts with
-  // the padded 400 / 144-B rows of the other modes)
-  static constexpr int AROW = MODE == 2 ? ME * EB : ME * EB + 16;  // bytes per A / H row
-  static constexpr int WROW = MODE == 2 ? 160 : MWROW;             // bytes per staged W row
+  static constexpr int AROW = ME * EB + 16;  // bytes per A / H row
+  static constexpr int WROW = MWROW;         // bytes per staged W row
   static constexpr int A_BYTES = MBM * AROW;
   static constexpr int W_BYTES = ME * WROW;
-  static constexpr int TOTAL = NP * (2 * A_BYTES + W_BYTES);
+  static constexpr int TOTAL = 2 * A_BYTES + W_BYTES;
   static constexpr int LN_BYTES = MBM * MLN_STRIDE * 4;
   static constexpr int BYTES = TOTAL > LN_BYTES ? TOTAL : LN_BYTES;
 };
 
-// byte offset of byte b of row r in an x3 A / H image
-__device__ __forceinline__ int x3_aoff(int r, int b) { return r * (ME * 2) + ((((b >> 4) ^ ((r >> 1) & 7))) << 4) + (b & 15); }
-
 template <int MODE>
-__global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float* __restrict__ X,
+__global__ __launch_bounds__(256, 2) void mlp_fused_kernel(float* __restrict__ X,
                                                                            const void* __restrict__ W1p,
                                                                            const void* __restrict__ W2p, int M, int Fh,
                                                                            float eps) {
-  constexpr bool BF16 = MODE != 0, X3 = MODE == 2;
+  constexpr bool BF16 = MODE != 0;
   using L = MlpLds<MODE>;
   constexpr int EB = L::EB;
   constexpr int BK = 128 / EB;          // K per W slice
@@ -57,12 +48,8 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
   unsigned char* As = smem;
   unsigned char* Hs = smem + L::A_BYTES;
   unsigned char* Ws = smem + 2 * L::A_BYTES;
-  unsigned char* Asl = smem + 2 * L::A_BYTES + L::W_BYTES;  // x3 lo planes
-  unsigned char* Hsl = Asl + L::A_BYTES;
-  unsigned char* Wsl = Hsl + L::A_BYTES;
   const unsigned char* W1 = (const unsigned char*)W1p;
   const unsigned char* W2 = (const unsigned char*)W2p;
-  const int64_t lo1 = X3 ? (int64_t)Fh * ME * 2 : 0, lo2 = lo1;  // bytes from a hi plane to its lo plane
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -76,13 +63,7 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
     const int64_t m = m0 + row;
     f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
     if (m < M) v = *(const f32x4*)(X + m * ME + c4 * 4);
-    if constexpr (X3) {
-      bf16x4 b, l;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) b[i] = (bf16)v[i], l[i] = (bf16)(v[i] - (float)b[i]);
-      *(bf16x4*)(As + x3_aoff(row, c4 * 8)) = b;
-      *(bf16x4*)(Asl + x3_aoff(row, c4 * 8)) = l;
-    } else if constexpr (BF16) {
+    if constexpr (BF16) {
       bf16x4 b;
       b[0] = (bf16)v[0]; b[1] = (bf16)v[1]; b[2] = (bf16)v[2]; b[3] = (bf16)v[3];
       *(bf16x4*)(As + row * L::AROW + c4 * 8) = b;
@@ -93,13 +74,12 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
 
   // ---- W slice staging (16-byte chunks, 6 per thread); a slice is 192 rows x 128 B
   constexpr int WCH = ME * 8 / 256;
-  u32x4 rw[WCH], rwl[X3 ? WCH : 1];
+  u32x4 rw[WCH];
   auto wload = [&](const unsigned char* base, int64_t ld_bytes) {
 #pragma unroll
     for (int j = 0; j < WCH; ++j) {
       const int cidx = tid + 256 * j;
       rw[j] = *(const u32x4*)(base + (cidx >> 3) * ld_bytes + (cidx & 7) * 16);
-      if constexpr (X3) rwl[j] = *(const u32x4*)(base + lo1 + (cidx >> 3) * ld_bytes + (cidx & 7) * 16);
     }
   };
   // W1 [Fh][E]: slice (c, ks) = rows c*192.., cols ks*BK..;  W2 [E][Fh]: rows 0..191, cols c*192 + ks*BK..
@@ -110,10 +90,9 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
     for (int j = 0; j < WCH; ++j) {
       const int cidx = tid + 256 * j;
       *(u32x4*)(Ws + (cidx >> 3) * L::WROW + (cidx & 7) * 16) = rw[j];
-      if constexpr (X3) *(u32x4*)(Wsl + (cidx >> 3) * L::WROW + (cidx & 7) * 16) = rwl[j];
     }
   };
-  (void)lo2;
+
 
   f32x4 accy[2][6], acch[2][6];
 #pragma unroll
@@ -125,28 +104,7 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int kb = ks * 128 + kk * 64 + fg * 16;  // byte offset inside the A/H row
-      if constexpr (X3) {
-        const unsigned char* Asl_ = Asrc == As ? Asl : Hsl;
-        bf16x8 af[2], afl[2], bw[6], bwl[6];
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          af[mt] = *(const bf16x8*)(Asrc + x3_aoff(wm * 32 + mt * 16 + fr, kb));
-          afl[mt] = *(const bf16x8*)(Asl_ + x3_aoff(wm * 32 + mt * 16 + fr, kb));
-        }
-#pragma unroll
-        for (int nt = 0; nt < 6; ++nt) {
-          bw[nt] = *(const bf16x8*)(Ws + (wn * 96 + nt * 16 + fr) * L::WROW + kk * 64 + fg * 16);
-          bwl[nt] = *(const bf16x8*)(Wsl + (wn * 96 + nt * 16 + fr) * L::WROW + kk * 64 + fg * 16);
-        }
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < 6; ++nt) {
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[mt], bw[nt], acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bwl[nt], acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bw[nt], acc[mt][nt], 0, 0, 0);
-          }
-      } else if constexpr (BF16) {
+      if constexpr (BF16) {
         bf16x8 af[2], bw[6];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) af[mt] = *(const bf16x8*)(Asrc + (wm * 32 + mt * 16 + fr) * L::AROW + kb);
@@ -196,12 +154,7 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
         for (int r = 0; r < 4; ++r) {
           const int rl = wm * 32 + mt * 16 + fg * 4 + r;
           const int cl = wn * 96 + nt * 16 + fr;
-          if constexpr (X3) {
-            const float g = gelu_erf(acch[mt][nt][r]);
-            const bf16 gh = (bf16)g;
-            *(bf16*)(Hs + x3_aoff(rl, cl * 2)) = gh;
-            *(bf16*)(Hsl + x3_aoff(rl, cl * 2)) = (bf16)(g - (float)gh);
-          } else if constexpr (BF16)
+          if constexpr (BF16)
             *(bf16*)(Hs + rl * L::AROW + cl * 2) = (bf16)gelu_tanh_fast(acch[mt][nt][r]);
           else
             *(float*)(Hs + rl * L::AROW + cl * 4) = gelu_erf(acch[mt][nt][r]);
@@ -269,6 +222,146 @@ __global__ __launch_bounds__(256, MODE == 2 ? 1 : 2) void mlp_fused_kernel(float
   }
 }
 
+// ---------------------------------------------------------------- parity mode, row-resident
+// PREC_F32 MLP sublayer with the layout of mlp_rows.hip (each wave keeps its 16 tokens in registers:
+// X^T as B fragments, the 192 x 16 Y^T accumulators initialised with the fp32 residual; H^T = W1c . X^T
+// per 32-hidden chunk, its GELU(erf) the B fragment of Y^T += W2c . H^T) on split-bf16 operands: X^T, H^T
+// and the weights as bf16 hi + lo, three products per contraction.  Only the weights go through LDS: a
+// chunk's W1 rows and W2 columns (hi and lo planes, 48 KB, XOR-swizzled for conflict-free ds_read_b128)
+// staged by registers once per 64-token block, so no activation moves through LDS and two waves share a
+// SIMD (the LDS-staged GEMM form of mlp_fused_kernel<2> ran one).
+constexpr int X3_HC = 32;                        // hidden chunk
+constexpr int X3_W1P = X3_HC * ME * 2;           // W1 chunk plane: 32 rows x 384 B
+constexpr int X3_W2P = ME * X3_HC * 2;           // W2 chunk plane: 192 rows x 64 B
+constexpr int X3_LDS = 2 * X3_W1P + 2 * X3_W2P;  // 48 KB
+
+__device__ __forceinline__ bf16x8 x3_hi(const f32x4& a, const f32x4& b, bf16x8& lo) {
+  bf16x8 hi;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    hi[i] = (bf16)a[i], hi[4 + i] = (bf16)b[i];
+    lo[i] = (bf16)(a[i] - (float)hi[i]), lo[4 + i] = (bf16)(b[i] - (float)hi[4 + i]);
+  }
+  return hi;
+}
+
+__global__ __launch_bounds__(256, 2) void mlp_x3_kernel(float* __restrict__ X, const bf16* __restrict__ W1,
+                                                        const bf16* __restrict__ W2p, int M, int Fh, float eps) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[X3_LDS];
+  unsigned char* W1h = lds;
+  unsigned char* W1l = lds + X3_W1P;
+  unsigned char* W2h = lds + 2 * X3_W1P;
+  unsigned char* W2l = W2h + X3_W2P;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * 64 + wave * 16;
+  const int64_t mrow = min(m0 + fr, (int64_t)M - 1);
+  const int nchunks = Fh / X3_HC;
+  const int64_t n1 = (int64_t)Fh * ME, n2 = n1;  // elements of one plane (W1 / W2)
+
+  // ---- staging: 3 units per thread and plane for W1 (rows c*32.., 24 units each) and W2 (192 rows x 4 units)
+  u32x4 s1h[3], s1l[3], s2h[3], s2l[3];
+  auto gload = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int q = tid + 256 * j;
+      const int r1 = q / 24, u1 = q % 24;
+      const bf16* a = W1 + ((int64_t)(c * X3_HC + r1) * ME + u1 * 8);
+      s1h[j] = *(const u32x4*)a, s1l[j] = *(const u32x4*)(a + n1);
+      const int r2 = q >> 2, u2 = q & 3;
+      const bf16* b = W2p + ((int64_t)r2 * Fh + c * X3_HC + u2 * 8);
+      s2h[j] = *(const u32x4*)b, s2l[j] = *(const u32x4*)(b + n2);
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int q = tid + 256 * j;
+      const int r1 = q / 24, u1 = q % 24;
+      const int o1 = r1 * 384 + ((u1 ^ ((r1 >> 1) & 7)) << 4);
+      *(u32x4*)(W1h + o1) = s1h[j], *(u32x4*)(W1l + o1) = s1l[j];
+      const int r2 = q >> 2, u2 = q & 3;
+      const int o2 = r2 * 64 + ((u2 ^ ((r2 >> 1) & 3)) << 4);
+      *(u32x4*)(W2h + o2) = s2h[j], *(u32x4*)(W2l + o2) = s2l[j];
+    }
+  };
+  gload(0);
+
+  // ---- the wave's 16 tokens: Y^T accumulators (residual) and X^T fragments (hi / lo)
+  f32x4 y[ME / 16];
+  bf16x8 xh[ME / 32], xl[ME / 32];
+  {
+    const float* xr = X + mrow * ME;
+#pragma unroll
+    for (int o = 0; o < ME / 16; ++o) y[o] = *(const f32x4*)(xr + 16 * o + 4 * fg);
+#pragma unroll
+    for (int ks = 0; ks < ME / 32; ++ks)
+      xh[ks] = x3_hi(*(const f32x4*)(xr + 32 * ks + 8 * fg), *(const f32x4*)(xr + 32 * ks + 8 * fg + 4), xl[ks]);
+  }
+  const int w1o = fr * 384, w1s = (fr >> 1) & 7;  // W1 fragment row 16 ht + fr (the swizzle ignores ht)
+  const int w2o = fr * 64 + ((fg ^ ((fr >> 1) & 3)) << 4);
+
+  for (int c = 0; c < nchunks; ++c) {
+    __syncthreads();  // every wave is done with chunk c-1's images
+    lstore();
+    __syncthreads();
+    if (c + 1 < nchunks) gload(c + 1);
+    // H^T [32 hidden][16 tokens] = W1c . X^T
+    f32x4 h[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < ME / 32; ++ks)
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht) {
+        const int off = ht * 16 * 384 + w1o + (((4 * ks + fg) ^ w1s) << 4);
+        const bf16x8 wh = *(const bf16x8*)(W1h + off), wl = *(const bf16x8*)(W1l + off);
+        h[ht] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xh[ks], h[ht], 0, 0, 0);
+        h[ht] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xl[ks], h[ht], 0, 0, 0);
+        h[ht] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh[ks], h[ht], 0, 0, 0);
+      }
+    // GELU(erf) -> B fragment of the down-projection: position 8fg + j <-> hidden (j < 4 ? 4fg + j : 16 + 4fg + j-4)
+    bf16x8 gh, gl;
+    {
+      f32x4 g0, g1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g0[i] = gelu_erf(h[0][i]), g1[i] = gelu_erf(h[1][i]);
+      gh = x3_hi(g0, g1, gl);
+    }
+    // Y^T [192][16 tokens] += W2c(perm) . GELU(H^T)
+#pragma unroll
+    for (int o = 0; o < ME / 16; ++o) {
+      const int off = o * 16 * 64 + w2o;
+      const bf16x8 wh = *(const bf16x8*)(W2h + off), wl = *(const bf16x8*)(W2l + off);
+      y[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, gh, y[o], 0, 0, 0);
+      y[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, gl, y[o], 0, 0, 0);
+      y[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, gh, y[o], 0, 0, 0);
+    }
+  }
+
+  // ---- residual (in y) + LayerNorm: lane = token fr, features 16o + 4fg + i
+  float sm = 0.f;
+#pragma unroll
+  for (int o = 0; o < ME / 16; ++o)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm += y[o][i];
+  const float mean = sum_rows4(sm) * (1.0f / ME);
+  float q = 0.f;
+#pragma unroll
+  for (int o = 0; o < ME / 16; ++o)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float dl = y[o][i] - mean;
+      q += dl * dl;
+    }
+  const float inv = 1.0f / sqrtf(sum_rows4(q) * (1.0f / ME) + eps);
+  if (m0 + fr < M) {
+    float* xo = X + (m0 + fr) * ME + 4 * fg;
+#pragma unroll
+    for (int o = 0; o < ME / 16; ++o)
+      *(f32x4*)(xo + 16 * o) =
+          f32x4{(y[o][0] - mean) * inv, (y[o][1] - mean) * inv, (y[o][2] - mean) * inv, (y[o][3] - mean) * inv};
+  }
+}
+
 }  // namespace
 
 hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M, int E, int Fh, float eps, int prec,
@@ -284,15 +377,13 @@ hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M,
     e = hipFuncSetAttribute((const void*)mlp_fused_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             MlpLds<0>::BYTES);
     if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)mlp_fused_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            MlpLds<2>::BYTES);
-    if (e != hipSuccess) return e;
     attr_set = true;
   }
   if (prec == PREC_BF16)
     hipLaunchKernelGGL(mlp_fused_kernel<1>, grid, dim3(256), MlpLds<1>::BYTES, st, X, W1, W2, (int)M, Fh, eps);
-  else if (prec == PREC_F32)  // W1 / W2: hi | lo planes
-    hipLaunchKernelGGL(mlp_fused_kernel<2>, grid, dim3(256), MlpLds<2>::BYTES, st, X, W1, W2, (int)M, Fh, eps);
+  else if (prec == PREC_F32)  // W1 natural, W2 in the pack_mlp2_perm order, each as hi | lo planes
+    hipLaunchKernelGGL(mlp_x3_kernel, dim3((unsigned)((M + 63) / 64)), dim3(256), 0, st, X, (const bf16*)W1,
+                       (const bf16*)W2, (int)M, Fh, eps);
   else
     hipLaunchKernelGGL(mlp_fused_kernel<0>, grid, dim3(256), MlpLds<0>::BYTES, st, X, W1, W2, (int)M, Fh, eps);
   return hipGetLastError();
