@@ -501,6 +501,22 @@ void setw(const mmpfn_ctx* ctx, GemmArgs& a, const DevBuf& f, const DevBuf& h, i
   }
 }
 
+// parity-mode row-resident projections (rowgemm3.hip): E = 192 = 6 heads of 32, split weights present
+bool proj3_ok(const mmpfn_ctx* ctx, int prec) {
+  return prec == PREC_F32 && ctx->d.emsize == 192 && ctx->d.nhead == 6;
+}
+Proj3Set p3set(const mmpfn_ctx* ctx, const DevBuf& f, const float* A, int64_t rdiv, int64_t rmul, int64_t rmul2,
+               int64_t roff, int64_t M, int N) {
+  const auto it = ctx->split.find(f.p);
+  Proj3Set s{A, rdiv, rmul, rmul2, roff, nullptr, 0, (int)M, N};
+  if (it != ctx->split.end()) s.W = it->second.p, s.w_lo = (int64_t)it->second.n;
+  return s;
+}
+hipError_t p3_resln(const mmpfn_ctx* ctx, const DevBuf& f, const void* O, int64_t M, float* X, hipStream_t st) {
+  const Proj3Set s = p3set(ctx, f, (const float*)O, 1, 1, 0, 0, M, 192);
+  return launch_proj3_resln(s.A, s.W, s.w_lo, M, X, ctx->d.ln_eps, st);
+}
+
 GemmArgs gargs() {
   GemmArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -631,13 +647,18 @@ int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int S, int T, in
     void* Qf = big;
     void* Kf = big + (size_t)R * E * eb;
     void* Vf = (unsigned char*)Kf + (size_t)S * H * Tpad * 32 * eb;
-    GemmArgs a = gargs();
     // logical rows m = s*T + t: A row t*S + s; scatter batch b = s, position t
-    a.A = X, a.lda = E, a.a_rdiv = T, a.a_rmul = 1, a.a_rmul2 = S;
-    setw(ctx, a, L.feat_qkv, L.feat_qkv_h, prec);
-    a.M = (int)R, a.N = 3 * E, a.K = E;
-    a.q = Qf, a.k = Kf, a.v = Vf, a.S = T, a.Npad = Tpad, a.T = T, a.H = H;
-    HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+    if (proj3_ok(ctx, prec)) {
+      const Proj3Set ps = p3set(ctx, L.feat_qkv, X, T, 1, S, 0, R, 3 * E);
+      HIPCHK(launch_proj3_qkv(&ps, 1, Qf, Kf, Vf, T, Tpad, H, st));
+    } else {
+      GemmArgs a = gargs();
+      a.A = X, a.lda = E, a.a_rdiv = T, a.a_rmul = 1, a.a_rmul2 = S;
+      setw(ctx, a, L.feat_qkv, L.feat_qkv_h, prec);
+      a.M = (int)R, a.N = 3 * E, a.K = E;
+      a.q = Qf, a.k = Kf, a.v = Vf, a.S = T, a.Npad = Tpad, a.T = T, a.H = H;
+      HIPCHK(launch_gemm(a, prec, EPI_ITEM_QKV, true, !bf, 1, st));
+    }
     AttnArgs f;
     f.q = Qf, f.k = Kf, f.vt = Vf, f.o = O;
     f.q_bstride = (int64_t)H * T * 32, f.q_hstride = (int64_t)T * 32;
@@ -645,6 +666,10 @@ int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int S, int T, in
     f.o_bstride = 1, f.o_qstride = S;  // O[t][s]
     f.s0 = 0, f.nq = T, f.nk = T, f.kvh_fixed = -1, f.H = H;
     HIPCHK(launch_attn(f, S, prec, 1, st));
+    if (proj3_ok(ctx, prec)) {
+      HIPCHK(p3_resln(ctx, L.feat_out, O, R, X, st));
+      continue;
+    }
     GemmArgs b = gargs();
     b.A = O, b.lda = E, setw(ctx, b, L.feat_out, L.feat_out_h, prec);
     b.M = (int)R, b.N = E, b.K = E, b.X = X, b.ln_eps = d.ln_eps;
@@ -679,6 +704,9 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
     const unsigned char* Vc = Kc + kvl;
     if (bf && E == 192) {
       HIPCHK(launch_rowgemm_qkv(Xall, S, S, 1, 0, L.item_qtest_h.p, TM * S, E, Qi, Ki, Vi, S, Npad, H, st));
+    } else if (proj3_ok(ctx, prec)) {
+      const Proj3Set ps = p3set(ctx, L.item_qtest, Xall, S, S, 1, 0, (int64_t)TM * S, E);
+      HIPCHK(launch_proj3_qkv(&ps, 1, Qi, Ki, Vi, S, Npad, H, st));
     } else {
       GemmArgs c = gargs();
       c.A = Xall, c.lda = E, c.a_rdiv = S, c.a_rmul = S, c.a_roff = 0;
@@ -697,6 +725,10 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
       // train rows q|k|v and test rows q in one launch (test-row blocks last)
       HIPCHK(launch_rowgemm_qkv_pair(Xall, N, 0, L.item_qkv_h.p, TM * N, 3 * E, Q, N, L.item_qtest_h.p, TM * Q, E, S,
                                      Qi, Ki, Vi, S, Npad, H, st));
+    } else if (proj3_ok(ctx, prec)) {  // train rows q|k|v and test rows q in one launch
+      const Proj3Set ps[2] = {p3set(ctx, L.item_qkv, Xall, N, S, 1, 0, (int64_t)TM * N, 3 * E),
+                              p3set(ctx, L.item_qtest, Xall, Q > 0 ? Q : 1, S, 1, N, (int64_t)TM * Q, E)};
+      HIPCHK(launch_proj3_qkv(ps, 2, Qi, Ki, Vi, S, Npad, H, st));
     } else {
       GemmArgs a = gargs();
       a.A = Xall, a.lda = E, a.a_rdiv = N, a.a_rmul = S, a.a_roff = 0;
@@ -746,6 +778,8 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
   if (fuse_out) return MMPFN_OK;
   if (bf && E == 192) {
     HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, RM, Xall, d.ln_eps, st));
+  } else if (proj3_ok(ctx, prec)) {
+    HIPCHK(p3_resln(ctx, L.item_out, O, RM, Xall, st));
   } else {
     GemmArgs b = gargs();
     b.A = O, b.lda = E, setw(ctx, b, L.item_out, L.item_out_h, prec);

@@ -89,6 +89,22 @@ hipError_t launch_rowgemm_ln_store(const float* A, const void* W, const float* b
                                    float eps, bool ln, hipStream_t st);
 hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, float* X, float eps, hipStream_t st);
 
+// parity-mode (x3 split-bf16) row-resident projections of width 192 (rowgemm3.hip), fp32 in and out:
+// W = the hi plane [N][192] of capi.cpp upsplit, its lo plane at W + w_lo elements.
+//   QKV: up to two row sets in one launch (same remap / scatter as launch_rowgemm_qkv, fp32 Q / K / V^T)
+//   RES_LN: X <- LN(X + O . W^T), O fp32 [M][192]
+struct Proj3Set {
+  const float* A;
+  int64_t a_rdiv, a_rmul, a_rmul2, a_roff;
+  const void* W;
+  int64_t w_lo;
+  int M, N;  // N = 576 (q | k | v) or 192 (q)
+};
+hipError_t launch_proj3_qkv(const Proj3Set* sets, int nset, void* q, void* k, void* vt, int S, int Npad, int H,
+                            hipStream_t st);
+hipError_t launch_proj3_resln(const float* O, const void* W, int64_t w_lo, int64_t M, float* X, float eps,
+                              hipStream_t st);
+
 // row-resident attention-between-features sublayer (bf16 only, featrow.hip): one wave per
 // table row, T <= 64 tokens; `pack` (capi.cpp pack_feat_rows) = LDS images with 416-B rows:
 // per head [96][FEAT_IMG_STRIDE] (Wq rows permuted & scaled by log2(e)/sqrt(32) | Wk rows

@@ -129,7 +129,7 @@ def test_shipped_library_is_the_production_build():
 
 
 @pytest.mark.parametrize("src,extra", [("attention.hip", ["-fno-honor-nans"]), ("gemm.hip", []), ("mlp_rows.hip", []),
-                                       ("rowgemm.hip", []), ("mlp.hip", [])])
+                                       ("rowgemm.hip", []), ("rowgemm3.hip", []), ("mlp.hip", [])])
 def test_hot_kernels_use_no_scratch(src, extra):
     """No private (scratch) segment in the hot kernels: an out-of-line lambda once sent the parity-mode
     attention's tile state through scratch (16.8 ms instead of 0.72 ms per launch) with zero reported spills."""

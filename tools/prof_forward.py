@@ -1,4 +1,4 @@
-"""Profiling driver: a few bf16 member forwards at the config-C shape (for rocprofv3 --pmc passes).
+"""Profiling driver: a few member forwards (bf16; MMPFN_PROF_PREC=f32: the parity mode) at the config-C shape (for rocprofv3 --pmc passes).
 
 Usage (on the GPU box):  rocprofv3 --pmc <counters> -d <dir> -o run --output-format csv -- \
                               python3 tools/prof_forward.py [n_forwards]
@@ -34,13 +34,14 @@ def main():
     x = torch.from_numpy(synth_table(S, 21, 2, n_cat=18)).cuda()
     im = torch.from_numpy(synth_image(S, 1, 2)).cuda()
     y = synth_labels(S, 6, 2)[:N]
-    tok = eng.mixer_tokens(im, _lib.PREC_BF16)
+    prec = _lib.PREC_F32 if os.environ.get("MMPFN_PROF_PREC") == "f32" else _lib.PREC_BF16
+    tok = eng.mixer_tokens(im, prec)
     batch = int(os.environ.get("MMPFN_PROF_BATCH", "1"))  # members per batched forward
     for _ in range(n):
         if batch > 1:
-            out = eng.forward_batch([(x, tok, y)] * batch, _lib.PREC_BF16)[0]
+            out = eng.forward_batch([(x, tok, y)] * batch, prec)[0]
         else:
-            out = eng.forward(x, tok, y, _lib.PREC_BF16, check_nan=False)
+            out = eng.forward(x, tok, y, prec, check_nan=False)
     eng.status()
     torch.cuda.synchronize()
     print("ok", tuple(out.shape), float(out.abs().mean()))
