@@ -202,6 +202,11 @@ int mmpfn_mlp_ln(mmpfn_ctx* ctx, int layer, float* X, int64_t rows, int precisio
 int mmpfn_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int precision);
 int mmpfn_cap(mmpfn_ctx* ctx, const float* mgm_tokens, int S, int M, float* tokens, int precision);
 
+/* Host helper of the predict path (no GPU, no context): the fingerprint feature's row hash
+ * (model/preprocessing.py:476-479, Python hash(row.tobytes()) under PYTHONHASHSEED=0 = SipHash-2-4 with the
+ * all-zero key, -1 mapped to -2).  rows: host, n_rows x row_bytes contiguous; out: host int64[n_rows]. */
+int mmpfn_siphash24_rows(const void* rows, int64_t n_rows, int64_t row_bytes, int64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

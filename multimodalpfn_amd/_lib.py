@@ -90,6 +90,7 @@ SIGNATURES = [
     ("mmpfn_cap", _i, [_vp, _vp, _i, _i, _vp, _i]),
     ("mmpfn_kernel_timing_read", _i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                       ctypes.POINTER(ctypes.c_double)]),
+    ("mmpfn_siphash24_rows", _i, [_vp, _i64, _i64, _vp]),
 ]
 
 # include/mmpfn_modality.h (modality encoders: DINOv2 ViT, ELECTRA text tower)

@@ -33,8 +33,40 @@ def _round(v0, v1, v2, v3):
     return v0, v1, v2, v3
 
 
+_NATIVE = None
+
+
+def _native():
+    """The library's ``mmpfn_siphash24_rows`` (host code, one pass over the bytes), or None where the
+    library cannot be loaded (host preprocessing also runs in CPU-only processes, e.g. ``fit``)."""
+    global _NATIVE
+    if _NATIVE is None:
+        try:
+            from multimodalpfn_amd import _lib
+
+            _NATIVE = _lib.load_library().mmpfn_siphash24_rows
+        except (OSError, RuntimeError, AttributeError):
+            _NATIVE = False
+    return _NATIVE or None
+
+
 def siphash24_rows(rows: np.ndarray) -> np.ndarray:
     """Python ``hash(row.tobytes())`` (zero secret) of each row of a 2-D array, as int64."""
+    rows = np.ascontiguousarray(rows)
+    fn = _native()
+    if fn is not None:
+        n = rows.shape[0]
+        out = np.empty(n, np.int64)
+        if n:
+            nb = rows.nbytes // n
+            if fn(rows.ctypes.data, n, nb, out.ctypes.data) != 0:
+                raise ValueError("mmpfn_siphash24_rows: bad arguments")
+        return out
+    return siphash24_rows_numpy(rows)
+
+
+def siphash24_rows_numpy(rows: np.ndarray) -> np.ndarray:
+    """The same hash in numpy ``uint64`` lanes (reference restatement; the fallback)."""
     rows = np.ascontiguousarray(rows)
     n = rows.shape[0]
     raw = rows.reshape(n, -1).view(np.uint8) if rows.size else np.zeros((n, 0), np.uint8)

@@ -116,6 +116,22 @@ def test_fingerprint_matches_python_hash_seed0():
     assert [int(v) for v in mine] == [int(v) for v in out]
 
 
+def test_native_row_hash_equals_the_numpy_restatement():
+    """The library's host hash (``mmpfn_siphash24_rows``) equals the numpy SipHash on every tail length."""
+    from multimodalpfn_amd.model import _siphash
+
+    if _siphash._native() is None:
+        pytest.skip("library not built")
+    rng = np.random.default_rng(5)
+    for nb in range(0, 41):
+        a = rng.integers(0, 256, (11, nb), dtype=np.uint8)
+        assert (_siphash.siphash24_rows(a) == _siphash.siphash24_rows_numpy(a)).all(), nb
+    a = rng.standard_normal((460, 36))
+    a[3] = a[2]
+    assert (_siphash.siphash24_rows(a) == _siphash.siphash24_rows_numpy(a)).all()
+    assert _siphash.siphash24_rows(np.zeros((0, 3))).shape == (0,)
+
+
 def test_interface_config_from_user_input():
     from multimodalpfn_amd.constants import ModelInterfaceConfig
 

@@ -16,7 +16,7 @@ HEADER = ROOT / "include" / "mmpfn_hip.h"
 
 def header_symbols():
     text = HEADER.read_text()
-    return sorted(set(re.findall(r"\b(mmpfn_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(mmpfn_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_header_matches_binding_table():
