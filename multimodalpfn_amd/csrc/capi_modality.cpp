@@ -266,7 +266,8 @@ int linear(mmpfn_enc* enc, int prec, const void* A, const Buf& Wf, const Buf& Wh
   g.a_rdiv = 1ll << 62, g.a_rmul = 0, g.a_rmul2 = 1, g.rdiv2 = 1ll << 62, g.ln_eps = 1e-5f;
   g.A = A, g.lda = K, g.W = Wf.p, g.bias = (const float*)bias.p, g.M = M, g.N = N, g.K = K, g.act = act;
   g.C = epi == GT_RESID ? (void*)Y : C, g.ldc = N;
-  HIPCHK(launch_gemm(g, PREC_F32, EPI_STORE, true, true, 1, enc->stream));
+  // the encoders' fp32 mode stays on fp32-input MFMA (their 1-2e-6 parity; the tower runs once per dataset)
+  HIPCHK(launch_gemm(g, PREC_F32_MFMA, EPI_STORE, true, true, 1, enc->stream));
   if (epi == GT_RESID) HIPCHK(launch_resid((float*)C, Y, gamma, M, N, enc->stream));
   return MMPFN_OK;
 }
