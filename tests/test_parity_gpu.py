@@ -47,6 +47,7 @@ def test_forward_fp32_matches_reference(case):
     z, meta, cfg, sd = load_case(case)
     out = run_case(z, make_model(cfg, sd))
     err = rel_err(out, z["logits"])
+    print(f"fp32 (split-bf16) {case}: rel err {err:.3e}")
     assert err <= F32_TOL, err
     assert (out.argmax(1) == z["logits"].argmax(1)).all()
 
@@ -57,7 +58,9 @@ def test_forward_fp32_input_mfma_mode_matches_reference(case, monkeypatch):
     monkeypatch.setenv("MMPFN_F32_MODE", "mfma")
     z, meta, cfg, sd = load_case(case)
     out = run_case(z, make_model(cfg, sd))
-    assert rel_err(out, z["logits"]) <= F32_TOL
+    err = rel_err(out, z["logits"])
+    print(f"fp32-input MFMA {case}: rel err {err:.3e}")
+    assert err <= F32_TOL, err
     assert (out.argmax(1) == z["logits"].argmax(1)).all()
 
 
