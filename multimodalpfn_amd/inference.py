@@ -40,8 +40,12 @@ def _precision(model, device: torch.device, autocast: bool, forced: torch.dtype 
 
 
 def _h2d(a, device: torch.device) -> torch.Tensor:
-    """fp32 host array -> device on the current stream."""
-    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(device)
+    """fp32 host array -> device on the current stream, through pinned memory and without a host wait (a
+    pageable copy is host-synchronous, so the launches that follow it would trail the GPU)."""
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
+    if device.type == "cuda":
+        return t.pin_memory().to(device, non_blocking=True)
+    return t.to(device)
 
 
 def _mixer_tokens(model, eng, image_train, image_test, prec: int, cache: dict | None = None):

@@ -1,4 +1,5 @@
-"""Diagnostic (GPU): where predict_proba's host time goes at config C (cProfile over 10 calls)."""
+"""Diagnostic (GPU): where predict_proba's host time goes at config C (cProfile over 10 calls; `default`: the
+reference's default member preprocessing)."""
 import cProfile
 import pstats
 import sys
@@ -23,16 +24,23 @@ with tempfile.TemporaryDirectory() as tmp:
     torch.save({"state_dict": {k: torch.from_numpy(v) for k, v in sd.items()}, "config": ckpt_config(cfg)}, ck)
     clf = MMPFNClassifier(model_path=str(ck), mixer_type="MGM+CAP", mgm_heads=64, cap_heads=24, features_per_group=2,
                           n_estimators=4, categorical_features_indices=list(range(18)), ignore_pretraining_limits=True,
-                          inference_config=ModelInterfaceConfig(FINGERPRINT_FEATURE=False,
-                                                                PREPROCESS_TRANSFORMS=[PreprocessorConfig(name="none")]))
+                          inference_config=(ModelInterfaceConfig() if "default" in sys.argv[1:] else
+                                            ModelInterfaceConfig(FINGERPRINT_FEATURE=False,
+                                                                 PREPROCESS_TRANSFORMS=[PreprocessorConfig(name="none")])))
     X = x.astype(np.float64)
     clf.fit(X[:1838], image[:1838], y[:1838].astype(np.int64))
 Xq, imq = X[1838:], image[1838:]
 for _ in range(3):
     clf.predict_proba(Xq, imq)
+import time  # noqa: E402
+t0 = time.perf_counter()
+for _ in range(10):
+    clf.predict_proba(Xq, imq)
+print("ms per predict", (time.perf_counter() - t0) * 100)
 pr = cProfile.Profile()
 pr.enable()
 for _ in range(10):
     clf.predict_proba(Xq, imq)
 pr.disable()
-pstats.Stats(pr).sort_stats("cumulative").print_stats(35)
+pstats.Stats(pr).sort_stats("cumulative").print_stats(45)
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)

@@ -4,7 +4,7 @@
 set -o pipefail
 R=$PWD; mkdir -p gpurun_out; export TMPDIR=/tmp
 for v in "$@"; do
-  lib=$R/multimodalpfn_amd/libmmpfn_var_$v.so; [ $v = main ] && lib=$R/multimodalpfn_amd/libmmpfn_hip.so
+  lib=$R/${VAR_DIR:-multimodalpfn_amd}/libmmpfn_var_$v.so; [ $v = main ] && lib=$R/multimodalpfn_amd/libmmpfn_hip.so
   cd /tmp || exit 1
   MMPFN_DIAGNOSTICS=1 MMPFN_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/kp_$v -o run --output-format csv -- \
     python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-modality --no-f32 --no-config-d --api-steps 0 \
