@@ -548,21 +548,6 @@ static_assert(A2_AHEAD == 1 || A2_SPT == 1, "prefetch depth 2 needs one tile per
 constexpr int A2_QPW = 32 * A2_NCH;  // queries per wave
 constexpr int A2_QPB = A2_NW * A2_QPW;
 
-struct Attn2Args {
-  const bf16* q;  // [B][H][S][32]
-  const bf16* k;  // [B][H][Npad][32]
-  const bf16* vt; // [B][H][32][Npad]
-  bf16* o;        // row b*S + s, element row*H*32 + h*32 + d
-  int S, H, Npad, nk;
-  int a0, na;          // own-head query rows
-  int b0, nb, kvb;     // shared-KV query rows (all heads) against kv head kvb
-  int tasks_per_b, nblocks;
-  int tstart[9];       // task prefix per kv head inside one column
-  int64_t kv_bstride;  // elements between the K (V^T) blocks of consecutive columns: H*Npad*32, or
-                       // Npad*32 for a head-0-only train-KV cache
-  int q_prescaled;     // Q already carries log2(e)/sqrt(32) (folded into the engine's bf16 Q weights)
-};
-
 __device__ __forceinline__ int a2_koff(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
 __device__ __forceinline__ int a2_voff(int d, int c) { return d * 128 + 16 * (c ^ ((d >> 1) & 7)); }
 
@@ -1369,6 +1354,11 @@ hipError_t launch_item_attention(const void* q, const void* k, const void* vt, v
 #ifdef MMPFN_ATTN_FP8PV
   hipLaunchKernelGGL(attn_item2_kernel<true>, dim3(a.nblocks), dim3(256), 0, st, a);
 #else
+  static const int pipe = [] {
+    const char* e = getenv("MMPFN_ATTN_PIPE");
+    return e ? atoi(e) : 0;
+  }();
+  if (pipe) return launch_attn_pipe(a, st);
   hipLaunchKernelGGL(attn_item2_kernel<false>, dim3(a.nblocks), dim3(256), 0, st, a);
 #endif
   return hipGetLastError();

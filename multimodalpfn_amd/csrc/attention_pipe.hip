@@ -1,0 +1,477 @@
+// Software-pipelined sample-axis attention for gfx950 (bf16): the item attention of one layer
+// (layer.py:341-379 attn_between_items; multi_head_attention.py:693-729), launch_attn_item2's task
+// map and numerics, re-shaped against the SIMD's issue model.
+//
+// At head dim 32 a 64x64 score tile of one wave costs 512 matrix-pipe cycles (16 MFMA-32) but
+// 64 v_exp_f32 (8 issue cycles each) + 32 v_cvt_pk_bf16_f32 + the MFMAs' issue holds: the SIMD's
+// issue port, not its matrix pipe, binds (~850 cycles per tile-wave).  attn_item2 leaves the two
+// waves of a SIMD to overlap that mix (measured ~1.4x the floor: each wave's exps wait on its own
+// S MFMAs, its P.V MFMAs on its own conversions, and a barrier per tile aligns the waves).  Here:
+//  * inside each wave a three-stage pipeline over (tile, 32-query chain) units:
+//    while the exps / conversions of unit j issue, the matrix pipe runs the S MFMAs of unit j+1
+//    and the P.V + row-sum MFMAs of unit j-1 -- nothing in a step waits on anything of the same
+//    step, and the step is one basic block whose order is pinned by sched_group_barrier;
+//  * K / V^T tiles staged once per block in a three-slot LDS ring (each thread one 16-B K and one
+//    16-B V^T chunk per tile, written a tile ahead, one s_barrier per tile with no vmcnt drain), the
+//    fragments read a step ahead of their MFMAs into two rotating register sets;
+//  * K rows are read in a permuted order (bits 2 and 3 of the row swapped), so the 8 keys a lane's
+//    P fragment holds are 8 consecutive keys: one 16-B V^T read per fragment, no permuted V^T image.
+// The softmax is attn_item2's: fixed reference 0 (Q carries log2(e)/sqrt(32)), p = exp2(s), row
+// sums on the MFMA pipe through a 0/1 selector, the sum range-checked per wave ([2^-60, 2^100)),
+// a wave out of range re-running with the first tile's row max, and an exact two-pass backstop.
+#include "common.h"
+#include "kernels.h"
+
+namespace mmpfn {
+
+namespace {
+
+constexpr int P4_KT = 64;    // keys per tile
+constexpr int P4_NCH = 2;    // 32-query chains per wave
+constexpr int P4_QPW = 32 * P4_NCH;
+constexpr int P4_QPB = 4 * P4_QPW;  // = launch_item_attention's 256 queries per task
+
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+
+// sched_group_barrier masks (LLVM AMDGPU IGroupLP)
+constexpr int SG_VALU = 0x2, SG_MFMA = 0x8, SG_VMEM_READ = 0x20, SG_DS_READ = 0x100, SG_DS_WRITE = 0x200,
+              SG_TRANS = 0x400;
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// exact two-pass softmax for one query per lane, K / V^T straight from global memory (backstop)
+__device__ __attribute__((noinline)) void p4_exact_rows(const Attn2Args& p, const bf16* Kg, const bf16* Vg,
+                                                        const bf16* qrow, bf16* orow, bool valid, float c) {
+  float q[32], o[32];
+#pragma unroll
+  for (int d = 0; d < 32; ++d) q[d] = (float)qrow[d] * c, o[d] = 0.f;
+  float m = -INFINITY;
+  for (int k = 0; k < p.nk; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) s = fmaf(q[d], (float)Kg[(int64_t)k * 32 + d], s);
+    m = fmaxf(m, s);
+  }
+  float l = 0.f;
+  for (int k = 0; k < p.nk; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) s = fmaf(q[d], (float)Kg[(int64_t)k * 32 + d], s);
+    const float e = exp2f(s - m);
+    l += e;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) o[d] = fmaf(e, (float)Vg[(int64_t)d * p.Npad + k], o[d]);
+  }
+  if (valid) {
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) orow[d] = (bf16)(o[d] * inv);
+  }
+}
+
+#ifndef P4_SLOT_BYTES
+#define P4_SLOT_BYTES 8192  // > 8192 pads the ring so that one block fills a CU (one wave per SIMD)
+#endif
+__global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[3][P4_SLOT_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+
+  // ---- task (attn_item2's map: contiguous task ranges per XCD, so one KV sequence stays in one L2)
+  int b, g, chunk;
+  {
+    const int nbk = p.nblocks, pid = blockIdx.x;
+    const int xcd = pid & 7, slot = pid >> 3;
+    const int task = xcd * (nbk >> 3) + min(xcd, nbk & 7) + slot;
+    b = task / p.tasks_per_b;
+    const int rem = task - b * p.tasks_per_b;
+    g = 0;
+    int base = p.tstart[0];
+#pragma unroll
+    for (int h = 1; h < 9; ++h)
+      if (h < p.H && p.tstart[h] <= rem) g = h, base = p.tstart[h];
+    chunk = rem - base;
+  }
+  const int cnt = p.na + (g == p.kvb ? p.H * p.nb : 0);
+  const int jw = chunk * P4_QPB + wave * P4_QPW;
+  const bool active = jw < cnt;  // wave-uniform; an idle wave still stages its share of every tile
+
+  const int64_t kvoff = (int64_t)b * p.kv_bstride + (int64_t)g * p.Npad * 32;
+  const bf16* Kg = p.k + kvoff;
+  const bf16* Vg = p.vt + kvoff;
+  const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
+
+  int qh[P4_NCH], qsrow[P4_NCH];
+  bool qok[P4_NCH];
+  bf16x8 qf[P4_NCH][2];
+#pragma unroll
+  for (int qb = 0; qb < P4_NCH; ++qb) {
+    const int j = jw + 32 * qb + r;
+    qok[qb] = j < cnt;
+    const int jc = min(j, cnt - 1);
+    if (jc < p.na) {
+      qh[qb] = g, qsrow[qb] = p.a0 + jc;
+    } else {
+      const int jj = jc - p.na;
+      qh[qb] = jj / p.nb, qsrow[qb] = p.b0 + jj % p.nb;
+    }
+    const bf16* qrow = p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 raw = *(const bf16x8*)(qrow + 16 * ks + 8 * hh);
+      if (p.q_prescaled) {
+        qf[qb][ks] = raw;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (bf16)((float)raw[e] * c);
+      }
+    }
+  }
+
+  const int ntiles = (p.nk + P4_KT - 1) / P4_KT;
+  const int nfull = p.nk / P4_KT;
+  const bool partial = nfull != ntiles;
+
+  // ---- fragments:
+  //   K   A operand of S^T = K Q^T : lane (r, hh) <- K[key 32u + pk(r)][16ks + 8hh .. +7], pk swapping
+  //       bits 2 and 3, so the S^T accumulator rows (i&3) + 8(i>>2) + 4hh of P fragment (u, sp) are the
+  //       keys 32u + 16sp + 8hh + 0..7
+  //   V^T A operand of O^T = V^T P^T: lane (r = d, hh) <- V^T[d][32u + 16sp + 8hh .. +7]
+  const int pkr = (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1);
+  // LDS ring: slot = K [64][32] (64-B rows) | V^T [32][64] (128-B rows), 16-B chunks XOR-swizzled
+  // (conflict-free ds_read_b128 for every 16-lane group, as attn_item2)
+  auto koff = [](int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); };
+  auto voff = [](int d, int c) { return 4096 + d * 128 + 16 * (c ^ ((d >> 1) & 7)); };
+  int kro[2][2], vro[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      kro[u][i] = koff(32 * u + pkr, 2 * i + hh);
+      vro[u][i] = voff(r, 4 * u + 2 * i + hh);
+    }
+  auto readk = [&](bf16x8(&kf)[2][2], const unsigned char* slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) kf[u][ks] = *(const bf16x8*)(slot + kro[u][ks]);
+  };
+  auto readv = [&](bf16x8(&vf)[2][2], const unsigned char* slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) vf[u][sp] = *(const bf16x8*)(slot + vro[u][sp]);
+  };
+  // staging: thread tid holds K row tid >> 2 chunk tid & 3 and V^T row tid >> 3 chunk tid & 7 of a tile
+  const int krow = tid >> 2, kc = tid & 3, vd = tid >> 3, vc = tid & 7;
+  const bf16* Ks = Kg + (int64_t)krow * 32 + kc * 8;
+  const bf16* Vs = Vg + (int64_t)vd * p.Npad + vc * 8;
+  const int kw = koff(krow, kc), vw = voff(vd, vc);
+  u32x4 rk, rv;
+  auto gload = [&](int t, u32x4& k, u32x4& v) __attribute__((always_inline)) {
+    k = *(const u32x4*)(Ks + (int64_t)t * (P4_KT * 32));
+    v = *(const u32x4*)(Vs + t * P4_KT);
+  };
+  auto lstore = [&](unsigned char* slot, const u32x4& k, const u32x4& v) __attribute__((always_inline)) {
+    *(u32x4*)(slot + kw) = k;
+    *(u32x4*)(slot + vw) = v;
+  };
+  // one barrier per tile: the LDS writes done (lgkmcnt(0)), global loads left in flight
+  auto lds_barrier = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // direct fragment loads (the non-pipelined tile below)
+  auto loadk = [&](bf16x8(&kf)[2][2], int t) __attribute__((always_inline)) {
+    const bf16* s = Kg + ((int64_t)t * P4_KT + pkr) * 32 + 8 * hh;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) kf[u][ks] = *(const bf16x8*)(s + u * 32 * 32 + 16 * ks);
+  };
+  auto loadv = [&](bf16x8(&vf)[2][2], int t) __attribute__((always_inline)) {
+    const bf16* s = Vg + (int64_t)r * p.Npad + t * P4_KT + 8 * hh;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) vf[u][sp] = *(const bf16x8*)(s + 32 * u + 16 * sp);
+  };
+
+  // row-sum selector (A of v_mfma_f32_16x16x32_bf16): D row 0 sums the P fragment's k-groups 0 and 2
+  // (queries 0-15 of the chain), row 1 k-groups 1 and 3 (queries 16-31)
+  bf16x8 sel;
+  {
+    const int m = lane & 15, kg = lane >> 4;
+    const bool one = (m == 0 && (kg & 1) == 0) || (m == 1 && (kg & 1) == 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sel[j] = (bf16)(one ? 1.0f : 0.0f);
+  }
+
+  f32x16 o[P4_NCH];
+  f32x4 lacc[P4_NCH];
+  auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int qb = 0; qb < P4_NCH; ++qb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[qb][i] = 0.f;
+      lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  zero_acc();
+
+  const f32x16 zero16 = {};
+  auto smm = [&](f32x16(&s)[2], const bf16x8(&kf)[2][2], int qb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      s[u] = mfma32(kf[u][0], qf[qb][0], zero16);
+      s[u] = mfma32(kf[u][1], qf[qb][1], s[u]);
+    }
+  };
+  auto expc = [&](bf16x8(&pb)[2][2], const f32x16(&s)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[u][sp][j] = (bf16)__builtin_amdgcn_exp2f(s[u][8 * sp + j]);
+  };
+  auto pv = [&](int qb, const bf16x8(&pb)[2][2], const bf16x8(&vf)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        o[qb] = mfma32(vf[u][sp], pb[u][sp], o[qb]);
+        lacc[qb] = mfma16(sel, pb[u][sp], lacc[qb]);
+      }
+  };
+  // the order of one pipeline step: 12 MFMAs (S0-S3 32x32, then P.V 32x32 / row-sum 16x16 pairs), 32
+  // exps, 16 conversions and the step's LDS / global traffic.  An MFMA holds vector issue for 8 cycles;
+  // a filler is free while the gap's issue sum fits the MFMA (32 / 16 cycles) and costs extra once it
+  // overflows (MI355X_MICROARCH.md constants), so each gap carries exactly its budget (P4_PIN 1: three
+  // exps per 32x32, one per 16x16) and the conversions + remaining exps follow in an MFMA-free tail
+#ifndef P4_PIN
+#define P4_PIN 1
+#endif
+  auto pin_step = [&](bool mem) __attribute__((always_inline)) {
+#if P4_PIN == 0
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+      if (mem) __builtin_amdgcn_sched_group_barrier(SG_DS_READ, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_TRANS, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_VALU, 1, 0);
+      if (mem && i == 1) __builtin_amdgcn_sched_group_barrier(SG_DS_WRITE, 2, 0);
+      if (mem && i == 2) __builtin_amdgcn_sched_group_barrier(SG_VMEM_READ, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_TRANS, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_VALU, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_TRANS, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_VALU, 2, 0);
+    }
+#else
+    // S MFMAs: 3 exps each (the LDS reads of the next fragments ride in the first two gaps)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+      if (mem && i < 2) __builtin_amdgcn_sched_group_barrier(SG_DS_READ, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_TRANS, 3, 0);
+    }
+    // P.V (32x32) + row-sum (16x16) pairs: 3 + 1 exps
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_TRANS, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_TRANS, P4_PIN == 2 ? 0 : 1, 0);
+    }
+    // tail: the remaining exps and the 16 conversions, then the staging traffic
+    __builtin_amdgcn_sched_group_barrier(SG_TRANS, P4_PIN == 2 ? 8 : 4, 0);
+    __builtin_amdgcn_sched_group_barrier(SG_VALU, 16, 0);
+    if (mem) {
+      __builtin_amdgcn_sched_group_barrier(SG_DS_WRITE, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_VMEM_READ, 2, 0);
+    }
+#endif
+  };
+
+  // ---- fast pass: fixed reference 0 over the full tiles, pipelined by (tile, chain) units
+  //   step (t, 0): S(t, chain 1) | exp S(t, chain 0) | P.V(t-1, chain 1); reads kf(t+1), vf(t) from LDS,
+  //                writes tile t+2 (staged) to LDS, loads tile t+3 into the staging registers
+  //   step (t, 1): S(t+1, chain 0) | exp S(t, chain 1) | P.V(t, chain 0); then the tile's barrier
+  // kf(t) in register set t % 2, vf(t) in set (t + 1) % 2; tile t in LDS slot t % 3
+  if (nfull > 0) {
+    bf16x8 kf[2][2][2], vf[2][2][2];
+    f32x16 sa[2], sb[2];
+    bf16x8 pa[2][2], pz[2][2];
+    {  // tiles 0 and 1 in flight together, then tile 2 into the staging registers
+      u32x4 rk1, rv1;
+      gload(0, rk, rv);
+      gload(min(1, ntiles - 1), rk1, rv1);
+      lstore(lds[0], rk, rv);
+      lstore(lds[1], rk1, rv1);
+    }
+    gload(min(2, ntiles - 1), rk, rv);
+    lds_barrier();
+    readk(kf[0], lds[0]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vf[0][u][sp][j] = pz[u][sp][j] = (bf16)0.0f;
+    smm(sa, kf[0], 0);
+    auto iter = [&](auto phc, auto slc, int t) __attribute__((always_inline)) {
+      constexpr int A = decltype(phc)::value, B = A ^ 1;
+      constexpr int L0 = decltype(slc)::value, L1 = (L0 + 1) % 3, L2 = (L0 + 2) % 3;
+      readk(kf[B], lds[L1]);
+      readv(vf[B], lds[L0]);
+      lstore(lds[L2], rk, rv);
+      gload(min(t + 3, ntiles - 1), rk, rv);
+      smm(sb, kf[A], 1);
+      expc(pa, sa);
+      pv(1, pz, vf[A]);
+      pin_step(true);
+      smm(sa, kf[B], 0);
+      expc(pz, sb);
+      pv(0, pa, vf[B]);
+      pin_step(false);
+      lds_barrier();
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    int t = 0;
+    for (; t + 6 <= nfull; t += 6) {
+      iter(I0{}, I0{}, t);
+      iter(I1{}, I1{}, t + 1);
+      iter(I0{}, I2{}, t + 2);
+      iter(I1{}, I0{}, t + 3);
+      iter(I0{}, I1{}, t + 4);
+      iter(I1{}, I2{}, t + 5);
+    }
+    // remaining 0-5 tiles: phase (t % 2, t % 3) with t % 6 == 0 here
+    if (t < nfull) iter(I0{}, I0{}, t++);
+    if (t < nfull) iter(I1{}, I1{}, t++);
+    if (t < nfull) iter(I0{}, I2{}, t++);
+    if (t < nfull) iter(I1{}, I0{}, t++);
+    if (t < nfull) iter(I0{}, I1{}, t++);
+    // drain: P.V of the last full tile's chain 1 (vf(nfull - 1) sits in set nfull % 2)
+    if (nfull & 1) pv(1, pz, vf[1]);
+    else pv(1, pz, vf[0]);
+  }
+
+  // ---- one tile, not pipelined: the partial last tile of the fast pass, and every tile of the
+  //      rare re-run with a reference (REF: s - mref; FIRST: mref = this tile's row max)
+  float mref[P4_NCH] = {0.f, 0.f};
+  auto tile1 = [&](int t, bool first, bool ref) {
+    const int k0 = t * P4_KT;
+    bf16x8 kf[2][2], vf[2][2];
+    loadk(kf, t);
+    loadv(vf, t);
+    const bool mask = k0 + P4_KT > p.nk;
+    if (mask) {  // keys >= nk: V = 0 so that p = 0 never meets NaN / inf padding
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (k0 + 32 * u + 16 * sp + 8 * hh + j >= p.nk) vf[u][sp][j] = (bf16)0.0f;
+    }
+#pragma unroll
+    for (int qb = 0; qb < P4_NCH; ++qb) {
+      f32x16 s[2];
+      smm(s, kf, qb);
+      if (mask) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (k0 + 32 * u + (i & 3) + 4 * ((i >> 2) & 1) + 8 * hh + 16 * (i >> 3) >= p.nk) s[u][i] = -INFINITY;
+      }
+      if (first) {
+        float m = fmaxf(s[0][0], s[1][0]);
+#pragma unroll
+        for (int i = 1; i < 16; ++i) m = fmaxf(m, fmaxf(s[0][i], s[1][i]));
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+        mref[qb] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      if (ref) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[0][i] -= mref[qb], s[1][i] -= mref[qb];
+      }
+      bf16x8 pb[2][2];
+      expc(pb, s);
+      pv(qb, pb, vf);
+    }
+  };
+  if (partial) tile1(nfull, false, false);
+
+  // the row sum of chain qb on the query's lanes (D rows 0 / 1 of lacc sit in lanes 0-15, registers 0 / 1)
+  auto rowsum = [&](int qb) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(lacc[qb][0]), __float_as_uint(lacc[qb][1]),
+                                                    false, false);
+    const auto s2 = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);
+    return __uint_as_float(s2[0]);
+  };
+  {  // reference-free pass out of [2^-60, 2^100) (tested on the bits; built with -fno-honor-nans) for
+     // any query of the wave: re-run the wave with the first tile's row max
+    bool bad = false;
+#pragma unroll
+    for (int qb = 0; qb < P4_NCH; ++qb) {
+      const unsigned lb = __float_as_uint(rowsum(qb)) & 0x7fffffffu;
+      bad |= lb >= 0x71800000u || lb < 0x21800000u;
+    }
+    if (__any(bad)) {
+      zero_acc();
+      for (int t = 0; t < ntiles; ++t) tile1(t, t == 0, true);
+    }
+  }
+
+  if (!active) return;
+  // ---- row sums to the query's lanes, overflow backstop, normalise, store
+#pragma unroll
+  for (int qb = 0; qb < P4_NCH; ++qb) {
+    const float ls = rowsum(qb);
+    bf16* orow = p.o + ((int64_t)b * p.S + qsrow[qb]) * (p.H * 32) + qh[qb] * 32;
+    if (__any((__float_as_uint(ls) & 0x7fffffffu) >= 0x71800000u)) {
+      const bf16* qrow = p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
+      p4_exact_rows(p, Kg, Vg, qrow, orow, qok[qb] && hh == 0, p.q_prescaled ? 1.0f : c);
+      continue;
+    }
+    const float inv = 1.0f / ls;
+    // lane (r, hh) holds d = 8 gq + 4 hh + 0..3: lanes 0-31 store d 8g .. 8g+7, lanes 32-63 d 8g+8 .. +15
+    u32x2 w[4];
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      bf16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (bf16)(o[qb][4 * gq + e] * inv);
+      w[gq] = __builtin_bit_cast(u32x2, v);
+    }
+#pragma unroll
+    for (int gg = 0; gg < 4; gg += 2) {
+      const auto sx = __builtin_amdgcn_permlane32_swap(w[gg].x, w[gg + 1].x, false, false);
+      const auto sy = __builtin_amdgcn_permlane32_swap(w[gg].y, w[gg + 1].y, false, false);
+      const u32x4 st = hh == 0 ? u32x4{w[gg].x, w[gg].y, sx[1], sy[1]} : u32x4{sx[0], sy[0], w[gg + 1].x, w[gg + 1].y};
+      if (qok[qb]) *(u32x4*)(orow + 8 * gg + 8 * hh) = st;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_attn_pipe(const Attn2Args& a, hipStream_t st) {
+  hipLaunchKernelGGL(attn_pipe_kernel, dim3(a.nblocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace mmpfn

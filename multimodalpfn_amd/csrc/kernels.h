@@ -135,6 +135,24 @@ struct AttnArgs {
   int s0, nq, nk, kvh_fixed, H;
 };
 hipError_t launch_attn(const AttnArgs& a, int batches, int prec, int waves_per_block, hipStream_t st);
+// task map + operands of the sample-axis attention kernels (attention.hip, attention_pipe.hip)
+struct Attn2Args {
+  const __bf16* q;  // [B][H][S][32]
+  const __bf16* k;  // [B][H][Npad][32]
+  const __bf16* vt; // [B][H][32][Npad]
+  __bf16* o;        // row b*S + s, element row*H*32 + h*32 + d
+  int S, H, Npad, nk;
+  int a0, na;          // own-head query rows
+  int b0, nb, kvb;     // shared-KV query rows (all heads) against kv head kvb
+  int tasks_per_b, nblocks;
+  int tstart[9];       // task prefix per kv head inside one column
+  int64_t kv_bstride;  // elements between the K (V^T) blocks of consecutive columns: H*Npad*32, or
+                       // Npad*32 for a head-0-only train-KV cache
+  int q_prescaled;     // Q already carries log2(e)/sqrt(32) (folded into the engine's bf16 Q weights)
+};
+// software-pipelined bf16 sample-axis attention (attention_pipe.hip): launch_attn_item2's task map and
+// semantics, one wave per SIMD, K / V^T fragments straight from L2 into registers
+hipError_t launch_attn_pipe(const Attn2Args& a, hipStream_t st);
 // bf16 sample-axis attention of one layer in one launch (attention.hip, attn_item2_kernel):
 //   own-head rows [a0, a0+na) of every head against that head's K/V, and rows [b0, b0+nb) of
 //   every head against K/V head kvb (nb = 0: none); keys [0, nk), Npad % 64 == 0.
