@@ -104,8 +104,8 @@ def attn_traffic(T):
     """HBM bytes per attention launch over T token columns, from the committed PMC pass
     (tools/attn_pmc.sh: rocprofv3 FETCH_SIZE and WRITE_SIZE runs at that launch shape)."""
     H, d, S, N = 6, 32, S_ROWS, N_TRAIN
-    for pmc in [*sorted((ROOT / "profiles" / "r02").glob("attn_item2_pmc_T*[0-9].json")),
-                *sorted((ROOT / "profiles" / "r01").glob("attn_item2_pmc*.json"))]:  # newest round first
+    # the shipped kernel's own pass only (attn_pipe_kernel from round 3; older rounds measured attn_item2)
+    for pmc in sorted((ROOT / "profiles" / "r03").glob("attn_pipe_pmc_T*[0-9].json")):
         rec = json.loads(pmc.read_text())
         if rec.get("shape") == {"T": T, "H": H, "d": d, "S": S, "N": N}:
             return rec["hbm_bytes_per_launch"], str(pmc.relative_to(ROOT))
@@ -114,7 +114,7 @@ def attn_traffic(T):
 
 def live_roofline(lib, ctx, T_launch):
     """Roofline of the dominant kernel from the launches INSIDE the timed region: HIP events
-    recorded by the engine on each lane's stream around every attn_item2 launch."""
+    recorded by the engine on each lane's stream around every item-attention launch."""
     import ctypes
 
     ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
@@ -135,7 +135,7 @@ def live_roofline(lib, ctx, T_launch):
         "traffic": traffic,
         "traffic_unit": f"HBM bytes per launch (PMC: 2 x FETCH_SIZE + WRITE_SIZE, {src})" if src else None,
         "algorithmic_bytes": 2 * T_launch * H * d * (S + 2 * N) + 2 * T_launch * S * H * d,
-        "kernel": "attn_item2_kernel (sample-axis attention: train + test-MQA rows of one layer, all members "
+        "kernel": "attn_pipe_kernel (sample-axis attention: train + test-MQA rows of one layer, all members "
                   "of a batched forward, per launch)",
         "launches_timed": n.value,
         "token_columns_per_launch": T_launch,
@@ -190,7 +190,7 @@ def time_item_attention(eng, T, reps, S=S_ROWS, N=N_TRAIN):
         "traffic": traffic,
         "traffic_unit": f"HBM bytes per launch (PMC: 2 x FETCH_SIZE + WRITE_SIZE, {src})" if src else None,
         "algorithmic_bytes": 2 * T * H * d * (S + 2 * N) + 2 * T * S * H * d,
-        "kernel": "attn_item2_kernel (sample-axis attention, train + test-MQA rows of one layer per launch)",
+        "kernel": "attn_pipe_kernel (sample-axis attention, train + test-MQA rows of one layer per launch)",
         "per_launch_ms": round(ms, 4),
         "per_launch_flop": flops,
     }

@@ -503,504 +503,8 @@ __global__ __launch_bounds__(256, 2) void attn_feat3_kernel(const AttnArgs p, in
   }
 }
 
-// ------------------------------------------------------------------ item attention v2 (bf16)
-// Sample-axis attention of one layer in ONE launch: the train rows against their own
-// head's K/V (layer.py:362-372) and the test rows of all heads against head 0's K/V
-// (multiquery_item_attention_for_test_set, layer.py:344-358) share the grid.  Work is
-// grouped by KV sequence (column b, kv head g): the queries that read (b, g) are
-//    own-head rows [a0, a0+na) of head g, then, for g == kvb, rows [b0, b0+nb) of all H heads,
-// cut into tasks of 256 queries = 4 waves x 64.  A block stages each 64-key K / V^T tile
-// once into LDS for its 4 waves; each wave runs two 32-query MFMA chains against it.
-//
-// Per 64-key tile and wave: 8 x v_mfma_f32_32x32x16_bf16 for S^T = K Q^T (query on the
-// lane), 8 for O^T += V^T P^T, 8 x v_mfma_f32_16x16x32_bf16 that sum P^T rows through a
-// 0/1 selector operand (the row sum never touches the VALU), 64 v_exp_f32 + 32 cvt_pk per
-// lane.  The softmax reference is FIXED: the first pass uses m = 0 (p = exp2(s) straight from the
-// S^T accumulator -- no max, no subtraction, every tile alike), the row sum l is checked once at
-// the end against [2^-60, 2^100) (it bounds every p from above, and p_max >= l / N from below), and
-// a block in which any query leaves that range re-runs its tile loop with m = the first tile's row
-// max, the S^T chains starting from the accumulator -m.  Scaling by a power of two is exact, so
-// either pass equals the running-max softmax up to rounding; keys more than ~60 below the row max
-// (log2 units) may flush to zero, 2^-60 of the max and less.  A wave whose second pass still
-// overflows (a score ~88 natural-log units past the first tile's max) recomputes its queries with
-// an exact two-pass softmax (a1_exact_rows).  Neither fallback is taken on model data; the
-// reference-free pass removes the first tile's max / subtract / reference moves (setup + first tile
-// 5.06 -> 4.07 us of a 37-us block at config C, -DA2_STAMPS).
-//
-// LDS images (no padding, XOR-swizzled 16-B chunks; conflict-free ds_read_b128 for the
-// four 16-lane groups of a wave, MI355X_MICROARCH.md LDS table):
-//   K   [64 keys][32 d]  64-B rows : chunk c of row k at k*64 + 16*(c ^ ((k >> 2) & 3))
-//   V^T [32 d][64 keys] 128-B rows : chunk c of row d at d*128 + 16*(c ^ ((d >> 1) & 7)), keys
-//        inside every 16-key group stored in the order 0-3, 8-11, 4-7, 12-15 so that the
-//        keys one lane owns in the S^T accumulator (4hh + {0-3, 8-11}) are one 16-B chunk.
-constexpr int A2_KT = 64;
-constexpr int A2_NW = 4;  // 8-wave (512-query) blocks measured slower: 363-372 vs 343 us at C, 1374 vs 1290 at E
-#ifndef A2_NCH
-#define A2_NCH 2  // 32-query MFMA chains per wave
-#endif
-#ifndef A2_SPT
-#define A2_SPT 1  // 64-key tiles per LDS stage (one barrier per stage)
-#endif
-#ifndef A2_AHEAD
-#define A2_AHEAD 1  // tiles in flight ahead of the one computed (2: two staging register sets, A2_SPT == 1)
-#endif
-static_assert(A2_AHEAD == 1 || A2_SPT == 1, "prefetch depth 2 needs one tile per stage");
-constexpr int A2_QPW = 32 * A2_NCH;  // queries per wave
-constexpr int A2_QPB = A2_NW * A2_QPW;
-
-__device__ __forceinline__ int a2_koff(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
-__device__ __forceinline__ int a2_voff(int d, int c) { return d * 128 + 16 * (c ^ ((d >> 1) & 7)); }
-
-// exact two-pass softmax for one query per lane, K / V^T straight from global memory
-__device__ __attribute__((noinline)) void a1_exact_rows(const Attn2Args& p, const bf16* Kg, const bf16* Vg,
-                                                         const bf16* qrow, bf16* orow, bool valid, float c) {
-  float q[32], o[32];  // c: the score scale still to apply to Q (log2(e)/sqrt(32), or 1 when prescaled)
-#pragma unroll
-  for (int d = 0; d < 32; ++d) q[d] = (float)qrow[d] * c, o[d] = 0.f;
-  float m = -INFINITY;
-  for (int k = 0; k < p.nk; ++k) {
-    float s = 0.f;
-#pragma unroll
-    for (int d = 0; d < 32; ++d) s = fmaf(q[d], (float)Kg[(int64_t)k * 32 + d], s);
-    m = fmaxf(m, s);
-  }
-  float l = 0.f;
-  for (int k = 0; k < p.nk; ++k) {
-    float s = 0.f;
-#pragma unroll
-    for (int d = 0; d < 32; ++d) s = fmaf(q[d], (float)Kg[(int64_t)k * 32 + d], s);
-    const float e = exp2f(s - m);
-    l += e;
-#pragma unroll
-    for (int d = 0; d < 32; ++d) o[d] = fmaf(e, (float)Vg[(int64_t)d * p.Npad + k], o[d]);
-  }
-  if (valid) {
-    const float inv = 1.0f / l;
-#pragma unroll
-    for (int d = 0; d < 32; ++d) orow[d] = (bf16)(o[d] * inv);
-  }
-}
-
-#ifndef A2_OCC
-#define A2_OCC (A2_NCH == 4 ? 1 : A2_NCH == 2 ? 2 : 3)  // waves per SIMD the register budget targets
-#endif
-// F8: P.V and the row sums on v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 P and V, unit block scales):
-// a measured A/B variant for the long-context config, not the default.  The V^T tile is
-// converted to e4m3 while staged and stored in the k order of the P fragment a lane builds from its
-// S^T accumulators (k = 32 hh + 16 u + r <-> key 32 u + (r & 3) + 8 (r >> 2) + 4 hh), 16-B chunks
-// XOR-swizzled by (d >> 2) & 3; the row sums come from the same instruction with a selector A
-// operand (rows 0 and 4 all ones), so they sum exactly the e4m3 weights the P.V product used.
-typedef __attribute__((ext_vector_type(8))) int i32x8;
-#ifdef A2_STAMPS  // diagnostics build: per-block timeline (tools/attn_stamps.py)
-__device__ unsigned long long a2_stamp_buf[16384 * 6];
-#define A2_STAMP(i) \
-  if (tid == 0 && blockIdx.x < 16384) a2_stamp_buf[blockIdx.x * 6 + (i)] = __builtin_amdgcn_s_memrealtime()
-#else
-#define A2_STAMP(i)
-#endif
-template <bool F8>
-__global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args p) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * A2_SPT][2 * 4096];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar task / activity tests
-  const int r = lane & 31, hh = lane >> 5;
-  A2_STAMP(0);
-
-  // ---- task: contiguous task ranges per XCD (blocks of one KV sequence share an L2)
-  int b, g, chunk;
-  {
-    const int nbk = p.nblocks, pid = blockIdx.x;
-    const int xcd = pid & 7, slot = pid >> 3;
-    const int task = xcd * (nbk >> 3) + min(xcd, nbk & 7) + slot;
-    b = task / p.tasks_per_b;
-    const int rem = task - b * p.tasks_per_b;
-    // g = the last head whose task prefix is <= rem (tstart is non-decreasing); constant indices, so
-    // the prefixes come with the other kernel arguments instead of a chain of dependent loads
-    g = 0;
-    int base = p.tstart[0];
-#pragma unroll
-    for (int h = 1; h < 9; ++h)
-      if (h < p.H && p.tstart[h] <= rem) g = h, base = p.tstart[h];
-    chunk = rem - base;
-  }
-  const int cnt = p.na + (g == p.kvb ? p.H * p.nb : 0);
-  const int jw = chunk * A2_QPB + wave * A2_QPW;  // first query of this wave
-  const bool active = jw < cnt;               // wave-uniform
-
-  const int64_t kvoff = (int64_t)b * p.kv_bstride + (int64_t)g * p.Npad * 32;
-  const bf16* Kg = p.k + kvoff;
-  const bf16* Vg = p.vt + kvoff;
-  const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
-
-  // ---- the lane's query of each 32-query chain
-  int qh[A2_NCH], qsrow[A2_NCH];
-  bool qok[A2_NCH];
-  bf16x8 qf[A2_NCH][2];
-#pragma unroll
-  for (int qb = 0; qb < A2_NCH; ++qb) {
-    const int j = jw + 32 * qb + r;
-    qok[qb] = j < cnt;
-    const int jc = min(j, cnt - 1);
-    if (jc < p.na) {
-      qh[qb] = g, qsrow[qb] = p.a0 + jc;
-    } else {
-      const int jj = jc - p.na;
-      qh[qb] = jj / p.nb, qsrow[qb] = p.b0 + jj % p.nb;
-    }
-    const bf16* qrow = p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 raw = *(const bf16x8*)(qrow + 16 * ks + 8 * hh);
-      if (p.q_prescaled) {
-        qf[qb][ks] = raw;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (bf16)((float)raw[e] * c);
-      }
-    }
-  }
-
-  const int ntiles = (p.nk + A2_KT - 1) / A2_KT;
-  const bool partial = (p.nk % A2_KT) != 0;
-
-  // ---- staging: one 16-B K chunk and one 16-B V^T chunk per thread and tile
-  const int krow = tid >> 2, kc = tid & 3;      // K tile [64][32]: row, chunk
-  const int vd = tid >> 3, vc = tid & 7;        // V^T tile [32][64]: row d, natural 8-key chunk
-  u32x4 rk[A2_SPT * A2_AHEAD], rv[A2_SPT * A2_AHEAD];
-  auto gload = [&](int u, int t) {  // tile t into staging registers u
-    const int k0 = t * A2_KT;
-    rk[u] = *(const u32x4*)(Kg + (int64_t)(k0 + krow) * 32 + kc * 8);
-    rv[u] = *(const u32x4*)(Vg + (int64_t)vd * p.Npad + k0 + vc * 8);
-    if (partial && t == ntiles - 1) {  // keys >= nk: V = 0 so that p = 0 never meets NaN / inf padding
-      bf16x8 e = __builtin_bit_cast(bf16x8, rv[u]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (k0 + vc * 8 + j >= p.nk) e[j] = (bf16)0.0f;
-      rv[u] = __builtin_bit_cast(u32x4, e);
-    }
-  };
-  const int koff_w = a2_koff(krow, kc);
-  const int voff_w0 = a2_voff(vd, vc & ~1) + 8 * (vc & 1), voff_w1 = a2_voff(vd, vc | 1) + 8 * (vc & 1);
-  // F8 V^T image: row vd (64 B), keys vc*8 .. +7 -> logical k 16u + 4q (+32 for the upper 4 keys)
-  const int f8_u = vc >> 2, f8_q = vc & 3;
-  const int f8_off0 = vd * 64 + 16 * ((f8_u) ^ ((vd >> 2) & 3)) + 4 * f8_q;       // k = 16u + 4q, chunk u
-  const int f8_off1 = vd * 64 + 16 * ((2 + f8_u) ^ ((vd >> 2) & 3)) + 4 * f8_q;   // k = 32 + 16u + 4q
-  auto lstore = [&](int u, int buf) {
-    unsigned char* Ks = lds[buf];
-    *(u32x4*)(Ks + koff_w) = rk[u];
-    if constexpr (F8) {
-      const bf16x8 e = __builtin_bit_cast(bf16x8, rv[u]);
-      int w0 = __builtin_amdgcn_cvt_pk_fp8_f32((float)e[0], (float)e[1], 0, false);
-      w0 = __builtin_amdgcn_cvt_pk_fp8_f32((float)e[2], (float)e[3], w0, true);
-      int w1 = __builtin_amdgcn_cvt_pk_fp8_f32((float)e[4], (float)e[5], 0, false);
-      w1 = __builtin_amdgcn_cvt_pk_fp8_f32((float)e[6], (float)e[7], w1, true);
-      *(int*)(Ks + 4096 + f8_off0) = w0;
-      *(int*)(Ks + 4096 + f8_off1) = w1;
-    } else {
-      *(u32x2*)(Ks + 4096 + voff_w0) = u32x2{rv[u].x, rv[u].y};
-      *(u32x2*)(Ks + 4096 + voff_w1) = u32x2{rv[u].z, rv[u].w};
-    }
-  };
-  // fragment read offsets (bytes inside a stage)
-  int kro[2][2], vro[2][2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      kro[u][i] = a2_koff(32 * u + r, 2 * i + hh);
-      vro[u][i] = 4096 + a2_voff(r, 2 * (2 * u + i) + hh);
-    }
-
-  // row-sum selector (A of v_mfma_f32_16x16x32_bf16): D row 0 sums k-groups 0 and 2 (queries
-  // 0-15 of the chain), row 1 sums k-groups 1 and 3 (queries 16-31); other rows zero.
-  bf16x8 sel;
-  {
-    const int m = lane & 15, kg = lane >> 4;
-    const bool one = (m == 0 && (kg & 1) == 0) || (m == 1 && (kg & 1) == 1);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sel[j] = (bf16)(one ? 1.0f : 0.0f);
-  }
-
-  f32x16 o[A2_NCH];
-  float mref[A2_NCH];  // the second pass's reference (first tile's row max), one register per chain
-  f32x4 lacc[A2_NCH];
-  f32x16 lacc8[F8 ? A2_NCH : 1];  // F8 row sums: D rows 0 and 4 (lanes 0-31 and 32-63, register 0)
-#pragma unroll
-  for (int qb = 0; qb < A2_NCH; ++qb) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) o[qb][i] = 0.f;
-    mref[qb] = 0.f;
-    lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int j = 0; j < (F8 ? A2_NCH : 1); ++j)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) lacc8[j][i] = 0.f;
-  i32x8 sel8;  // e4m3 selector: A rows 0 and 4 all ones (0x38 = 1.0)
-  {
-    const int ones = ((lane & 31) == 0 || (lane & 31) == 4) ? 0x38383838 : 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sel8[j] = ones;
-  }
-
-  // REF: the second pass (scores minus the first tile's row max, subtracted on the VALU: that pass
-  // is rare, and keeping -m as an MFMA accumulator operand would hold 16 registers per chain)
-  auto tile = [&](int it, auto maskc, auto firstc, auto parc, auto refc) {
-    constexpr bool MASK = decltype(maskc)::value;
-    constexpr bool FIRST = decltype(firstc)::value;
-    constexpr bool REF = decltype(refc)::value;
-    const f32x16 zero16 = {};
-    constexpr int PAR = decltype(parc)::value;  // it & 1 (A2_AHEAD == 2: the staging set / LDS slot)
-    const int k0 = it * A2_KT;
-    const int sub = it % A2_SPT;  // position inside the stage of A2_SPT tiles
-#if A2_AHEAD == 2
-    if (it + 2 < ntiles) gload(PAR, it + 2);  // set PAR held tile it, staged at the last barrier
-    const unsigned char* Ks = lds[PAR];
-#else
-    if (sub == 0)
-#pragma unroll
-      for (int u = 0; u < A2_SPT; ++u)
-        if (it + A2_SPT + u < ntiles) gload(u, it + A2_SPT + u);
-    const unsigned char* Ks = lds[it % (2 * A2_SPT)];
-#endif
-    if (active) {
-      bf16x8 kf[2][2], vf[2][2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          kf[u][i] = *(const bf16x8*)(Ks + kro[u][i]);
-          if constexpr (!F8) vf[u][i] = *(const bf16x8*)(Ks + vro[u][i]);
-        }
-      f32x16 s[A2_NCH][2];
-#pragma unroll
-      for (int qb = 0; qb < A2_NCH; ++qb)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qf[qb][0], zero16, 0, 0, 0);
-          s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][1], qf[qb][1], s[qb][u], 0, 0, 0);
-        }
-      if constexpr (MASK) {
-#pragma unroll
-        for (int qb = 0; qb < A2_NCH; ++qb)
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-              if (k0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * hh >= p.nk) s[qb][u][i] = -INFINITY;
-      }
-      if constexpr (FIRST) {  // fix the reference max per query: this tile's row max (second pass)
-#pragma unroll
-        for (int qb = 0; qb < A2_NCH; ++qb) {
-          float m = fmaxf(s[qb][0][0], s[qb][1][0]);
-#pragma unroll
-          for (int i = 1; i < 16; ++i) m = fmaxf(m, fmaxf(s[qb][0][i], s[qb][1][i]));
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
-          m = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-          mref[qb] = m;
-        }
-      }
-      if constexpr (REF) {
-#pragma unroll
-        for (int qb = 0; qb < A2_NCH; ++qb)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            s[qb][0][i] -= mref[qb];
-            s[qb][1][i] -= mref[qb];
-          }
-      }
-      if constexpr (F8) {
-        const unsigned char* Vs8 = Ks + 4096 + r * 64;
-        const int sw = (r >> 2) & 3;
-        const u32x4 v0 = *(const u32x4*)(Vs8 + 16 * ((2 * hh) ^ sw));
-        const u32x4 v1 = *(const u32x4*)(Vs8 + 16 * ((2 * hh + 1) ^ sw));
-        const i32x8 va = i32x8{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
-#pragma unroll
-        for (int qb = 0; qb < A2_NCH; ++qb) {
-          i32x8 pf;
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-              int x = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_exp2f(s[qb][u][4 * w]),
-                                                      __builtin_amdgcn_exp2f(s[qb][u][4 * w + 1]), 0, false);
-              x = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_exp2f(s[qb][u][4 * w + 2]),
-                                                  __builtin_amdgcn_exp2f(s[qb][u][4 * w + 3]), x, true);
-              pf[4 * u + w] = x;
-            }
-          o[qb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(va, pf, o[qb], 0, 0, 0, 127, 0, 127);
-          lacc8[qb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(sel8, pf, lacc8[qb], 0, 0, 0, 127, 0, 127);
-        }
-      } else
-#pragma unroll
-      for (int qb = 0; qb < A2_NCH; ++qb)
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int sp = 0; sp < 2; ++sp) {
-            bf16x8 pb;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) pb[j] = (bf16)__builtin_amdgcn_exp2f(s[qb][u][8 * sp + j]);
-            o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[u][sp], pb, o[qb], 0, 0, 0);
-            lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[qb], 0, 0, 0);
-          }
-    }
-#if A2_AHEAD == 2
-    // tile it+1 (loaded a tile ago) goes to the slot tile it-1 used: every wave left it at the last barrier
-    if (it + 1 < ntiles) lstore(PAR ^ 1, PAR ^ 1);
-    __syncthreads();
-    (void)sub;
-#else
-    (void)PAR;
-    if (sub == A2_SPT - 1) {  // end of a stage: the next stage's tiles go to the other half of the ring
-#pragma unroll
-      for (int u = 0; u < A2_SPT; ++u)
-        if (it + 1 + u < ntiles) lstore(u, (it + 1 + u) % (2 * A2_SPT));
-      __syncthreads();
-    }
-#endif
-  };
-
-#if A2_AHEAD == 2
-  gload(0, 0);
-  if (ntiles > 1) gload(1, 1);
-  lstore(0, 0);
-#else
-#pragma unroll
-  for (int u = 0; u < A2_SPT; ++u)
-    if (u < ntiles) gload(u, u);
-#pragma unroll
-  for (int u = 0; u < A2_SPT; ++u)
-    if (u < ntiles) lstore(u, u);
-#endif
-  __syncthreads();
-  A2_STAMP(1);
-  using P0 = std::integral_constant<int, 0>;
-  using P1 [[maybe_unused]] = std::integral_constant<int, 1>;
-  using Y = std::true_type;
-  using N = std::false_type;
-  // one pass over the key tiles; WM: the first tile fixes the reference (row max), else m = 0
-  auto pass = [&](auto wmc) {
-    constexpr bool WM = decltype(wmc)::value;
-    using F = std::integral_constant<bool, WM>;
-    if (ntiles == 1) {
-      if (partial) tile(0, Y{}, F{}, P0{}, F{});
-      else tile(0, N{}, F{}, P0{}, F{});
-    } else {
-      tile(0, N{}, F{}, P0{}, F{});
-      A2_STAMP(2);
-      const int nfull = p.nk / A2_KT;
-#if A2_AHEAD == 2
-      int it = 1;
-      for (; it + 1 < nfull; it += 2) {
-        tile(it, N{}, N{}, P1{}, F{});
-        tile(it + 1, N{}, N{}, P0{}, F{});
-      }
-      if (it < nfull) tile(it++, N{}, N{}, P1{}, F{});
-      if (partial) {
-        if (it & 1) tile(it, Y{}, N{}, P1{}, F{});
-        else tile(it, Y{}, N{}, P0{}, F{});
-      }
-#else
-      for (int it = 1; it < nfull; ++it) tile(it, N{}, N{}, P0{}, F{});
-      if (partial) tile(nfull, Y{}, N{}, P0{}, F{});
-#endif
-    }
-  };
-  // the row sum of chain qb on the query's lanes
-  auto rowsum = [&](int qb) {
-    if constexpr (F8) {
-      return lacc8[qb][0];
-    } else {
-      // D rows 0 / 1 (queries 0-15 / 16-31) sit in lanes 0-15, registers 0 / 1
-      const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(lacc[qb][0]), __float_as_uint(lacc[qb][1]),
-                                                      false, false);  // lanes 16-31 <- register 1 of 0-15
-      const auto s2 = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);  // lanes 32-63 <- 0-31
-      return __uint_as_float(s2[0]);
-    }
-  };
-  pass(N{});
-  A2_STAMP(3);
-  {  // reference-free pass out of range ([2^-60, 2^100), tested on the bits; this file builds with
-     // -fno-honor-nans) for any query of the block: all waves re-run with the first tile's max
-    bool bad = false;
-    if (active)
-#pragma unroll
-      for (int qb = 0; qb < A2_NCH; ++qb) {
-        const unsigned lb = __float_as_uint(rowsum(qb)) & 0x7fffffffu;
-        bad |= lb >= 0x71800000u || lb < 0x21800000u;
-      }
-    const int any_bad = __syncthreads_or(bad ? 1 : 0);
-    if (any_bad) {
-#pragma unroll
-      for (int qb = 0; qb < A2_NCH; ++qb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[qb][i] = 0.f;
-        lacc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int j = 0; j < (F8 ? A2_NCH : 1); ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) lacc8[j][i] = 0.f;
-#if A2_AHEAD == 2
-      gload(0, 0);
-      if (ntiles > 1) gload(1, 1);
-      lstore(0, 0);
-#else
-#pragma unroll
-      for (int u = 0; u < A2_SPT; ++u)
-        if (u < ntiles) gload(u, u);
-#pragma unroll
-      for (int u = 0; u < A2_SPT; ++u)
-        if (u < ntiles) lstore(u, u);
-#endif
-      __syncthreads();
-      pass(Y{});
-    }
-  }
-  if (!active) return;
-
-  // ---- row sums to the query's lanes, overflow backstop, normalise, store
-#pragma unroll
-  for (int qb = 0; qb < A2_NCH; ++qb) {
-    const float ls = rowsum(qb);
-    bf16* orow = p.o + ((int64_t)b * p.S + qsrow[qb]) * (p.H * 32) + qh[qb] * 32;
-    // some p overflowed the fixed reference (sum >= 2^100, inf or NaN -- tested on the bits:
-    // this file builds with -fno-honor-nans): exact recompute
-    if (__any((__float_as_uint(ls) & 0x7fffffffu) >= 0x71800000u)) {
-      const bf16* qrow = p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
-      // lanes 0-31 own the chain's 32 queries; lanes 32-63 duplicate them and do not store
-      a1_exact_rows(p, Kg, Vg, qrow, orow, qok[qb] && hh == 0, p.q_prescaled ? 1.0f : c);
-      continue;
-    }
-    const float inv = 1.0f / ls;
-    // lane (r, hh) holds d = 8 gq + 4 hh + 0..3; permlane32_swap(a, b) gives lanes 32-63 the b of lanes
-    // 0-31 (first result) and lanes 0-31 the a of lanes 32-63 (second): 16-B stores of d 8g .. 8g+7
-    // (lanes 0-31) and 8g+8 .. 8g+15 (lanes 32-63), g = 0, 2
-    u32x2 w[4];
-#pragma unroll
-    for (int gq = 0; gq < 4; ++gq) {
-      bf16x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (bf16)(o[qb][4 * gq + e] * inv);
-      w[gq] = __builtin_bit_cast(u32x2, v);
-    }
-#pragma unroll
-    for (int g = 0; g < 4; g += 2) {
-      const auto sx = __builtin_amdgcn_permlane32_swap(w[g].x, w[g + 1].x, false, false);
-      const auto sy = __builtin_amdgcn_permlane32_swap(w[g].y, w[g + 1].y, false, false);
-      const u32x4 st = hh == 0 ? u32x4{w[g].x, w[g].y, sx[1], sy[1]} : u32x4{sx[0], sy[0], w[g + 1].x, w[g + 1].y};
-      if (qok[qb]) *(u32x4*)(orow + 8 * g + 8 * hh) = st;
-    }
-  }
-#ifdef A2_STAMPS
-  A2_STAMP(4);
-  if (tid == 0 && blockIdx.x < 16384) a2_stamp_buf[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-#endif
-}
-
 // ------------------------------------------------------------------ item attention, parity mode
-// PREC_F32: attn_item2's task map, LDS images and fixed-reference softmax on fp32 Q / K / V^T, every
+// PREC_F32: the bf16 kernel's task map (attention_pipe.hip) and fixed-reference softmax on fp32 Q / K / V^T, every
 // operand split into bf16 hi + lo planes (x = hi + lo to 2^-17): Q in registers, K / V^T as they are
 // staged into LDS (two planes per image), and P = exp2(S) in registers.  Per 64-key tile and chain
 //   S^T = Kl Qh + Kh Ql + Kh Qh          (6 x v_mfma_f32_32x32x16_bf16 per 32 keys)
@@ -1008,6 +512,15 @@ __global__ __launch_bounds__(256, A2_OCC) void attn_item2_kernel(const Attn2Args
 // in fp32 accumulators: each product carries the operands to 2^-16, so the attention matches the
 // exact fp32 softmax to ~1e-5 relative at three bf16 MFMAs where fp32-input MFMA takes sixteen.
 // Output O is fp32 ([row][H*32], the out-projection's A).
+// LDS images of a 64-key tile (unpadded, XOR-swizzled 16-B chunks; conflict-free ds_read_b128 for the
+// four 16-lane groups of a wave):
+//   K   [64 keys][32 d]  64-B rows : chunk c of row k at k*64 + 16*(c ^ ((k >> 2) & 3))
+//   V^T [32 d][64 keys] 128-B rows : chunk c of row d at d*128 + 16*(c ^ ((d >> 1) & 7)), keys inside every
+//        16-key group stored in the order 0-3, 8-11, 4-7, 12-15 so that the keys one lane owns in the S^T
+//        accumulator (4hh + {0-3, 8-11}) are one 16-B chunk
+constexpr int A2_KT = 64;
+__device__ __forceinline__ int a2_koff(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
+__device__ __forceinline__ int a2_voff(int d, int c) { return d * 128 + 16 * (c ^ ((d >> 1) & 7)); }
 constexpr int A3_NCH = 2;
 constexpr int A3_QPW = 32 * A3_NCH;
 constexpr int A3_QPB = 4 * A3_QPW;
@@ -1058,7 +571,7 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
 
-  int b, g, chunk;  // task map of attn_item2 (contiguous task ranges per XCD)
+  int b, g, chunk;  // task map of attn_pipe_kernel (contiguous task ranges per XCD)
   {
     const int nbk = p.nblocks, pid = blockIdx.x;
     const int xcd = pid & 7, slot = pid >> 3;
@@ -1144,7 +657,7 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
       kro[u][i] = a2_koff(32 * u + r, 2 * i + hh);
       vro[u][i] = 8192 + a2_voff(r, 2 * (2 * u + i) + hh);
     }
-  bf16x8 sel;  // row-sum selector (attn_item2)
+  bf16x8 sel;  // row-sum selector (attn_pipe_kernel)
   {
     const int m = lane & 15, kg = lane >> 4;
     const bool one = (m == 0 && (kg & 1) == 0) || (m == 1 && (kg & 1) == 1);
@@ -1313,11 +826,6 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
 
 }  // namespace
 
-#ifdef A2_STAMPS
-extern "C" int mmpfn_dbg_attn_stamps(void* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(a2_stamp_buf), sizeof(a2_stamp_buf));
-}
-#endif
 
 namespace {
 hipError_t launch_item_attention(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
@@ -1332,11 +840,8 @@ hipError_t launch_item_attention(const void* q, const void* k, const void* vt, v
   a.a0 = a0, a.na = na, a.b0 = b0, a.nb = nb, a.kvb = nb > 0 ? kvb : -1;
   a.kv_bstride = kv_bstride > 0 ? kv_bstride : (int64_t)H * Npad * 32;
   a.q_prescaled = q_prescaled ? 1 : 0;
-#ifdef A2_STAMPS  // diagnostics: time the engine's prescaled-Q prologue through the raw tap
-  if (getenv("A2_STAMPS_PRESCALED")) a.q_prescaled = 1;
-#endif
   if (kv_bstride > 0 && (na > 0 || kvb != 0)) return hipErrorInvalidValue;  // cache layout holds head 0 only
-  const int qpb = x3 ? A3_QPB : A2_QPB;
+  const int qpb = x3 ? A3_QPB : ATTN_ITEM_QPB;
   int acc = 0;
   for (int g = 0; g < H; ++g) {
     a.tstart[g] = acc;
@@ -1351,22 +856,12 @@ hipError_t launch_item_attention(const void* q, const void* k, const void* vt, v
     hipLaunchKernelGGL(attn_item3_kernel, dim3(a.nblocks), dim3(256), 0, st, a);
     return hipGetLastError();
   }
-#ifdef MMPFN_ATTN_FP8PV
-  hipLaunchKernelGGL(attn_item2_kernel<true>, dim3(a.nblocks), dim3(256), 0, st, a);
-#else
-  static const int pipe = [] {
-    const char* e = getenv("MMPFN_ATTN_PIPE");
-    return e ? atoi(e) : 0;
-  }();
-  if (pipe) return launch_attn_pipe(a, st);
-  hipLaunchKernelGGL(attn_item2_kernel<false>, dim3(a.nblocks), dim3(256), 0, st, a);
-#endif
-  return hipGetLastError();
+  return launch_attn_pipe(a, st);
 }
 
 }  // namespace
 
-hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
+hipError_t launch_attn_layer(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride,
                              bool q_prescaled) {
   return launch_item_attention(q, k, vt, out, S, T, H, Npad, nk, a0, na, b0, nb, kvb, st, kv_bstride, q_prescaled,

@@ -1,22 +1,24 @@
 // Software-pipelined sample-axis attention for gfx950 (bf16): the item attention of one layer
-// (layer.py:341-379 attn_between_items; multi_head_attention.py:693-729), launch_attn_item2's task
-// map and numerics, re-shaped against the SIMD's issue model.
+// (layer.py:341-379 attn_between_items; multi_head_attention.py:693-729) in ONE launch per layer: the
+// train rows against their own head's K/V (layer.py:362-372) and the test rows of all heads against
+// head 0's K/V (multiquery_item_attention_for_test_set, layer.py:344-358), re-shaped against the SIMD's
+// issue model.
 //
 // At head dim 32 a 64x64 score tile of one wave costs 512 matrix-pipe cycles (16 MFMA-32) but
 // 64 v_exp_f32 (8 issue cycles each) + 32 v_cvt_pk_bf16_f32 + the MFMAs' issue holds: the SIMD's
-// issue port, not its matrix pipe, binds (~850 cycles per tile-wave).  attn_item2 leaves the two
-// waves of a SIMD to overlap that mix (measured ~1.4x the floor: each wave's exps wait on its own
-// S MFMAs, its P.V MFMAs on its own conversions, and a barrier per tile aligns the waves).  Here:
+// issue port, not its matrix pipe, binds (~850 cycles per tile-wave).  Round 2's kernel left the two
+// waves of a SIMD to overlap that mix (measured ~1.5x the floor: each wave's exps wait on its own
+// S MFMAs, its P.V MFMAs on its own conversions).  Here:
 //  * inside each wave a three-stage pipeline over (tile, 32-query chain) units:
 //    while the exps / conversions of unit j issue, the matrix pipe runs the S MFMAs of unit j+1
 //    and the P.V + row-sum MFMAs of unit j-1 -- nothing in a step waits on anything of the same
 //    step, and the step is one basic block whose order is pinned by sched_group_barrier;
-//  * K / V^T tiles staged once per block in a three-slot LDS ring (each thread one 16-B K and one
+//  * K / V^T tiles staged once per block in a four-slot LDS ring (each thread one 16-B K and one
 //    16-B V^T chunk per tile, written a tile ahead, one s_barrier per tile with no vmcnt drain), the
 //    fragments read a step ahead of their MFMAs into two rotating register sets;
 //  * K rows are read in a permuted order (bits 2 and 3 of the row swapped), so the 8 keys a lane's
 //    P fragment holds are 8 consecutive keys: one 16-B V^T read per fragment, no permuted V^T image.
-// The softmax is attn_item2's: fixed reference 0 (Q carries log2(e)/sqrt(32)), p = exp2(s), row
+// Softmax: fixed reference 0 (Q carries log2(e)/sqrt(32)), p = exp2(s), row
 // sums on the MFMA pipe through a 0/1 selector, the sum range-checked per wave ([2^-60, 2^100)),
 // a wave out of range re-running with the first tile's row max, and an exact two-pass backstop.
 #include "common.h"
@@ -29,7 +31,8 @@ namespace {
 constexpr int P4_KT = 64;    // keys per tile
 constexpr int P4_NCH = 2;    // 32-query chains per wave
 constexpr int P4_QPW = 32 * P4_NCH;
-constexpr int P4_QPB = 4 * P4_QPW;  // = launch_item_attention's 256 queries per task
+constexpr int P4_QPB = 4 * P4_QPW;
+static_assert(P4_QPB == ATTN_ITEM_QPB, "launch_item_attention's task size");
 
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
 
@@ -75,15 +78,17 @@ __device__ __attribute__((noinline)) void p4_exact_rows(const Attn2Args& p, cons
 }
 
 #ifndef P4_SLOT_BYTES
-#define P4_SLOT_BYTES 8192  // > 8192 pads the ring so that one block fills a CU (one wave per SIMD)
+#define P4_SLOT_BYTES (64 * 80 + 32 * 144)
 #endif
 __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[3][P4_SLOT_BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned char ring[4 * P4_SLOT_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
 
-  // ---- task (attn_item2's map: contiguous task ranges per XCD, so one KV sequence stays in one L2)
+  // ---- task: the queries that read KV sequence (column b, kv head g) are the own-head rows [a0, a0+na)
+  //      of head g, then, for g == kvb, rows [b0, b0+nb) of all H heads, cut into tasks of 256 (4 waves
+  //      x 64); contiguous task ranges per XCD, so one KV sequence stays in one L2
   int b, g, chunk;
   {
     const int nbk = p.nblocks, pid = blockIdx.x;
@@ -107,21 +112,29 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   const bf16* Vg = p.vt + kvoff;
   const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
 
-  int qh[P4_NCH], qsrow[P4_NCH];
-  bool qok[P4_NCH];
+  // the lane's query of chain qb: head and table row (recomputed after the tile loop rather than kept live)
+  struct QRow {
+    int h, s;
+    bool ok;
+  };
+  auto qrow_of = [&](int qb) __attribute__((always_inline)) {
+    const int j = jw + 32 * qb + r;
+    const int jc = min(j, cnt - 1);
+    QRow q;
+    q.ok = j < cnt;
+    if (jc < p.na) {
+      q.h = g, q.s = p.a0 + jc;
+    } else {
+      const int jj = jc - p.na;
+      q.h = jj / p.nb, q.s = p.b0 + jj % p.nb;
+    }
+    return q;
+  };
   bf16x8 qf[P4_NCH][2];
 #pragma unroll
   for (int qb = 0; qb < P4_NCH; ++qb) {
-    const int j = jw + 32 * qb + r;
-    qok[qb] = j < cnt;
-    const int jc = min(j, cnt - 1);
-    if (jc < p.na) {
-      qh[qb] = g, qsrow[qb] = p.a0 + jc;
-    } else {
-      const int jj = jc - p.na;
-      qh[qb] = jj / p.nb, qsrow[qb] = p.b0 + jj % p.nb;
-    }
-    const bf16* qrow = p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
+    const QRow q = qrow_of(qb);
+    const bf16* qrow = p.q + (((int64_t)b * p.H + q.h) * p.S + q.s) * 32;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 raw = *(const bf16x8*)(qrow + 16 * ks + 8 * hh);
@@ -144,17 +157,18 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   //       keys 32u + 16sp + 8hh + 0..7
   //   V^T A operand of O^T = V^T P^T: lane (r = d, hh) <- V^T[d][32u + 16sp + 8hh .. +7]
   const int pkr = (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1);
-  // LDS ring: slot = K [64][32] (64-B rows) | V^T [32][64] (128-B rows), 16-B chunks XOR-swizzled
-  // (conflict-free ds_read_b128 for every 16-lane group, as attn_item2)
-  auto koff = [](int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); };
-  auto voff = [](int d, int c) { return 4096 + d * 128 + 16 * (c ^ ((d >> 1) & 7)); };
+  // LDS ring: slot = K [64][32] in 80-B rows | V^T [32][64] in 144-B rows: the padded strides make the
+  // ds_read_b128 of every 16-lane group conflict-free (row * 20 and d * 36 dwords are distinct mod 64
+  // over 16 rows), and every fragment of a lane sits at one base + an immediate offset
+  constexpr int KROW = 80, VROW = 144, VBASE = 64 * KROW;
+  const int kb = (32 * 0 + pkr) * KROW + 16 * hh, vb = VBASE + r * VROW + 16 * hh;
   int kro[2][2], vro[2][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      kro[u][i] = koff(32 * u + pkr, 2 * i + hh);
-      vro[u][i] = voff(r, 4 * u + 2 * i + hh);
+      kro[u][i] = kb + 32 * u * KROW + 32 * i;
+      vro[u][i] = vb + 64 * u + 32 * i;
     }
   auto readk = [&](bf16x8(&kf)[2][2], const unsigned char* slot) __attribute__((always_inline)) {
 #pragma unroll
@@ -170,13 +184,12 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   };
   // staging: thread tid holds K row tid >> 2 chunk tid & 3 and V^T row tid >> 3 chunk tid & 7 of a tile
   const int krow = tid >> 2, kc = tid & 3, vd = tid >> 3, vc = tid & 7;
-  const bf16* Ks = Kg + (int64_t)krow * 32 + kc * 8;
-  const bf16* Vs = Vg + (int64_t)vd * p.Npad + vc * 8;
-  const int kw = koff(krow, kc), vw = voff(vd, vc);
+  const int kso = krow * 32 + kc * 8, vso = vd * p.Npad + vc * 8;  // 32-bit lane offsets on wave-uniform bases
+  const int kw = krow * KROW + 16 * kc, vw = VBASE + vd * VROW + 16 * vc;
   u32x4 rk, rv;
   auto gload = [&](int t, u32x4& k, u32x4& v) __attribute__((always_inline)) {
-    k = *(const u32x4*)(Ks + (int64_t)t * (P4_KT * 32));
-    v = *(const u32x4*)(Vs + t * P4_KT);
+    k = *(const u32x4*)(Kg + (int64_t)t * (P4_KT * 32) + kso);
+    v = *(const u32x4*)(Vg + t * P4_KT + vso);
   };
   auto lstore = [&](unsigned char* slot, const u32x4& k, const u32x4& v) __attribute__((always_inline)) {
     *(u32x4*)(slot + kw) = k;
@@ -306,7 +319,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   //   step (t, 0): S(t, chain 1) | exp S(t, chain 0) | P.V(t-1, chain 1); reads kf(t+1), vf(t) from LDS,
   //                writes tile t+2 (staged) to LDS, loads tile t+3 into the staging registers
   //   step (t, 1): S(t+1, chain 0) | exp S(t, chain 1) | P.V(t, chain 0); then the tile's barrier
-  // kf(t) in register set t % 2, vf(t) in set (t + 1) % 2; tile t in LDS slot t % 3
+  // kf(t) in register set t % 2, vf(t) in set (t + 1) % 2
   if (nfull > 0) {
     bf16x8 kf[2][2][2], vf[2][2][2];
     f32x16 sa[2], sb[2];
@@ -315,12 +328,12 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       u32x4 rk1, rv1;
       gload(0, rk, rv);
       gload(min(1, ntiles - 1), rk1, rv1);
-      lstore(lds[0], rk, rv);
-      lstore(lds[1], rk1, rv1);
+      lstore(ring, rk, rv);
+      lstore(ring + P4_SLOT_BYTES, rk1, rv1);
     }
     gload(min(2, ntiles - 1), rk, rv);
     lds_barrier();
-    readk(kf[0], lds[0]);
+    readk(kf[0], ring);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -328,12 +341,13 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) vf[0][u][sp][j] = pz[u][sp][j] = (bf16)0.0f;
     smm(sa, kf[0], 0);
-    auto iter = [&](auto phc, auto slc, int t) __attribute__((always_inline)) {
-      constexpr int A = decltype(phc)::value, B = A ^ 1;
-      constexpr int L0 = decltype(slc)::value, L1 = (L0 + 1) % 3, L2 = (L0 + 2) % 3;
-      readk(kf[B], lds[L1]);
-      readv(vf[B], lds[L0]);
-      lstore(lds[L2], rk, rv);
+    // tile t in ring slot t % 4 (compile-time slots: every LDS address is a base + an immediate)
+    auto iter = [&](auto phc, int t) __attribute__((always_inline)) {
+      constexpr int L = decltype(phc)::value, A = L & 1, B = A ^ 1;
+      constexpr int S0 = L * P4_SLOT_BYTES, S1 = ((L + 1) & 3) * P4_SLOT_BYTES, S2 = ((L + 2) & 3) * P4_SLOT_BYTES;
+      readk(kf[B], ring + S1);
+      readv(vf[B], ring + S0);
+      lstore(ring + S2, rk, rv);
       gload(min(t + 3, ntiles - 1), rk, rv);
       smm(sb, kf[A], 1);
       expc(pa, sa);
@@ -348,21 +362,17 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
     int t = 0;
-    for (; t + 6 <= nfull; t += 6) {
-      iter(I0{}, I0{}, t);
-      iter(I1{}, I1{}, t + 1);
-      iter(I0{}, I2{}, t + 2);
-      iter(I1{}, I0{}, t + 3);
-      iter(I0{}, I1{}, t + 4);
-      iter(I1{}, I2{}, t + 5);
+    for (; t + 4 <= nfull; t += 4) {
+      iter(I0{}, t);
+      iter(I1{}, t + 1);
+      iter(I2{}, t + 2);
+      iter(I3{}, t + 3);
     }
-    // remaining 0-5 tiles: phase (t % 2, t % 3) with t % 6 == 0 here
-    if (t < nfull) iter(I0{}, I0{}, t++);
-    if (t < nfull) iter(I1{}, I1{}, t++);
-    if (t < nfull) iter(I0{}, I2{}, t++);
-    if (t < nfull) iter(I1{}, I0{}, t++);
-    if (t < nfull) iter(I0{}, I1{}, t++);
+    if (t < nfull) iter(I0{}, t++);
+    if (t < nfull) iter(I1{}, t++);
+    if (t < nfull) iter(I2{}, t++);
     // drain: P.V of the last full tile's chain 1 (vf(nfull - 1) sits in set nfull % 2)
     if (nfull & 1) pv(1, pz, vf[1]);
     else pv(1, pz, vf[0]);
@@ -441,10 +451,11 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
 #pragma unroll
   for (int qb = 0; qb < P4_NCH; ++qb) {
     const float ls = rowsum(qb);
-    bf16* orow = p.o + ((int64_t)b * p.S + qsrow[qb]) * (p.H * 32) + qh[qb] * 32;
+    const QRow q = qrow_of(qb);
+    bf16* orow = p.o + ((int64_t)b * p.S + q.s) * (p.H * 32) + q.h * 32;
     if (__any((__float_as_uint(ls) & 0x7fffffffu) >= 0x71800000u)) {
-      const bf16* qrow = p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
-      p4_exact_rows(p, Kg, Vg, qrow, orow, qok[qb] && hh == 0, p.q_prescaled ? 1.0f : c);
+      const bf16* qrow = p.q + (((int64_t)b * p.H + q.h) * p.S + q.s) * 32;
+      p4_exact_rows(p, Kg, Vg, qrow, orow, q.ok && hh == 0, p.q_prescaled ? 1.0f : c);
       continue;
     }
     const float inv = 1.0f / ls;
@@ -462,7 +473,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       const auto sx = __builtin_amdgcn_permlane32_swap(w[gg].x, w[gg + 1].x, false, false);
       const auto sy = __builtin_amdgcn_permlane32_swap(w[gg].y, w[gg + 1].y, false, false);
       const u32x4 st = hh == 0 ? u32x4{w[gg].x, w[gg].y, sx[1], sy[1]} : u32x4{sx[0], sy[0], w[gg + 1].x, w[gg + 1].y};
-      if (qok[qb]) *(u32x4*)(orow + 8 * gg + 8 * hh) = st;
+      if (q.ok) *(u32x4*)(orow + 8 * gg + 8 * hh) = st;
     }
   }
 }

@@ -98,7 +98,7 @@ struct mmpfn_ctx {
   std::vector<Lane> lanes;  // lanes[cur] is stale while cur is selected
   int cur = 0;
   // live timing of the sample-axis attention launches (mmpfn_kernel_timing): HIP events
-  // recorded on the launching stream around every attn_item2 launch while enabled
+  // recorded on the launching stream around every item-attention launch while enabled
   mmpfn_cache* cache_out = nullptr;       // being built by the current forward (train rows only)
   const mmpfn_cache* cache_in = nullptr;  // used by the current forward (test rows only)
   bool kt_on = false;
@@ -336,7 +336,7 @@ int finalize(mmpfn_ctx* ctx) {
     if ((rc = upload(ctx, L.item_qtest, wtest, false))) return rc;
     if ((rc = upsplit(ctx, L.item_qkv, wtrain))) return rc;
     if ((rc = upsplit(ctx, L.item_qtest, wtest))) return rc;
-    // bf16 copies: the Q rows carry the attention kernel's log2(e)/sqrt(32) (attn_item2 with
+    // bf16 copies: the Q rows carry the attention kernel's log2(e)/sqrt(32) (attn_pipe_kernel with
     // q_prescaled: no per-query scaling pass; one bf16 rounding of Q instead of two)
     const float qsc = 1.4426950408889634f / std::sqrt((float)(E / d.nhead));
     for (size_t i = 0; i < (size_t)HD * E; ++i) wtrain[i] *= qsc;
@@ -717,7 +717,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
     }
     const int64_t cstride = (int64_t)cc->Npad * 32;
     if (bf)
-      HIPCHK(launch_attn_item2(Qi, Kc, Vc, O, S, TM, H, cc->Npad, cc->N, 0, 0, 0, S, 0, st, cstride, true));
+      HIPCHK(launch_attn_layer(Qi, Kc, Vc, O, S, TM, H, cc->Npad, cc->N, 0, 0, 0, S, 0, st, cstride, true));
     else
       HIPCHK(launch_attn_item(Qi, Kc, Vc, O, S, TM, H, cc->Npad, 0, S, cc->N, 0, prec, st, cstride));
   } else {
@@ -766,7 +766,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
         ctx->kt_flops += 4.0 * TM * (double)(N + Q) * N * E;
         HIPCHK(hipEventRecord(ev[0], st));
       }
-      HIPCHK(launch_attn_item2(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st, 0, true));
+      HIPCHK(launch_attn_layer(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st, 0, true));
       if (ev) HIPCHK(hipEventRecord(ev[1], st));
     } else if (prec == PREC_F32) {  // parity mode: split-bf16 products, train and test rows in one launch
       HIPCHK(launch_attn_item3(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st));
@@ -1290,7 +1290,7 @@ int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, con
   if (N <= 0 || N > S || N > Npad || Npad % 64 || H <= 0 || H > 8 || T <= 0)
     return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
   HIPCHK(hipSetDevice(ctx->device));
-  HIPCHK(launch_attn_item2(q, k, vt, out, S, T, H, Npad, N, 0, N, N, S - N, 0, ctx->stream));
+  HIPCHK(launch_attn_layer(q, k, vt, out, S, T, H, Npad, N, 0, N, N, S - N, 0, ctx->stream));
   return MMPFN_OK;
 }
 

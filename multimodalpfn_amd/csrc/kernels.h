@@ -150,18 +150,18 @@ struct Attn2Args {
                        // Npad*32 for a head-0-only train-KV cache
   int q_prescaled;     // Q already carries log2(e)/sqrt(32) (folded into the engine's bf16 Q weights)
 };
-// software-pipelined bf16 sample-axis attention (attention_pipe.hip): launch_attn_item2's task map and
-// semantics, one wave per SIMD, K / V^T fragments straight from L2 into registers
+// software-pipelined bf16 sample-axis attention (attention_pipe.hip); tasks of ATTN_ITEM_QPB queries
+constexpr int ATTN_ITEM_QPB = 256;
 hipError_t launch_attn_pipe(const Attn2Args& a, hipStream_t st);
-// bf16 sample-axis attention of one layer in one launch (attention.hip, attn_item2_kernel):
+// bf16 sample-axis attention of one layer in one launch (attention_pipe.hip, attn_pipe_kernel):
 //   own-head rows [a0, a0+na) of every head against that head's K/V, and rows [b0, b0+nb) of
 //   every head against K/V head kvb (nb = 0: none); keys [0, nk), Npad % 64 == 0.
 //   kv_bstride > 0: K / V^T hold head 0 only, column blocks kv_bstride elements apart (train-KV
 //   cache; then na = 0 and kvb = 0)
-hipError_t launch_attn_item2(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
+hipError_t launch_attn_layer(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0,
                              bool q_prescaled = false);  // Q already scaled by log2(e)/sqrt(32)
-// parity mode (PREC_F32) of launch_attn_item2 on fp32 Q / K / V^T (split bf16 three-product MFMAs), fp32 O
+// parity mode (PREC_F32) of launch_attn_layer on fp32 Q / K / V^T (split bf16 three-product MFMAs), fp32 O
 hipError_t launch_attn_item3(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0);
 // item attention: queries s in [s0, s0+nq), keys [0, nk); kv_head_fixed >= 0 forces that KV head

@@ -1,4 +1,4 @@
-"""Per-launch HBM bytes of attn_item2_kernel from two rocprofv3 --pmc runs (FETCH_SIZE, WRITE_SIZE).
+"""Per-launch HBM bytes of attn_pipe_kernel from two rocprofv3 --pmc runs (FETCH_SIZE, WRITE_SIZE).
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  On gfx950 FETCH_SIZE counts half the bytes of a
 16-B-per-lane streaming read (MI355X_MICROARCH.md, HBM section): the kernel's K, V^T and Q reads
@@ -14,7 +14,7 @@ NPAD = (N + 63) // 64 * 64
 vals = {}
 for path in sys.argv[1:]:
     for r in csv.DictReader(open(f"{path}/run_counter_collection.csv")):
-        if "attn_item2_kernel" in r["Kernel_Name"]:
+        if "attn_pipe_kernel" in r["Kernel_Name"]:
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
 write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
@@ -23,7 +23,7 @@ write_b = write * 1024
 alg_read = T * H * S * d * 2 + 2 * T * H * N * d * 2  # Q + K + V^T (bf16), keys up to nk
 alg_write = T * S * H * d * 2
 print(json.dumps({
-    "kernel": "attn_item2_kernel",
+    "kernel": "attn_pipe_kernel",
     "shape": {"T": T, "H": H, "d": d, "S": S, "N": N},
     "launches": len(vals["FETCH_SIZE"]),
     "FETCH_SIZE_KiB_avg": round(fetch, 1),

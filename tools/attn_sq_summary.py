@@ -1,4 +1,4 @@
-"""Summarise tools/attn_sq_pmc.sh: per-dispatch SQ / GRBM counters of attn_item2_kernel (sums over
+"""Summarise tools/attn_sq_pmc.sh: per-dispatch SQ / GRBM counters of the item-attention kernel (KSEL) (sums over
 the kernel's dispatches divided by their count), plus derived ratios."""
 import collections
 import csv
@@ -11,7 +11,7 @@ acc = collections.defaultdict(float)
 disp = collections.defaultdict(set)
 for f in sorted(root.glob("*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if os.environ.get("KSEL", "attn_item2") not in r["Kernel_Name"]:
+        if os.environ.get("KSEL", "attn_pipe") not in r["Kernel_Name"]:
             continue
         acc[r["Counter_Name"]] += float(r["Counter_Value"])
         disp[r["Counter_Name"]].add(r.get("Dispatch_Id", r.get("Correlation_Id")))
