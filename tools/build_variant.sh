@@ -7,8 +7,9 @@ name=$1; flags=$2
 C=multimodalpfn_amd/csrc
 B=/tmp/mmpfn_var_$name
 mkdir -p $B
-for src in capi.cpp gemm.hip attention.hip encoder.hip mixer.hip mlp.hip mlp_rows.hip featblock.hip featrow.hip rowgemm.hip rowgemm3.hip modality.hip capi_modality.cpp host.cpp; do
-  extra=""; { [ $src = attention.hip ] || [ $src = featrow.hip ]; } && extra="-fno-honor-nans"
+srcs=$(sed -n '/^SRCS :=/,/^OBJS/p' $C/Makefile | grep -v '^OBJS' | sed 's/SRCS :=//; s/\\//g')
+for src in $srcs; do
+  extra=""; { [ $src = attention.hip ] || [ $src = attention_pipe.hip ] || [ $src = featrow.hip ]; } && extra="-fno-honor-nans"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -mllvm -amdgpu-mfma-vgpr-form=1 \
     $extra $flags -x hip -c $C/$src -o $B/$src.o &
 done

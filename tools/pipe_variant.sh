@@ -7,7 +7,7 @@ name=$1; script=$2; flags=$3
 D=${VAR_DIR:-abvar}; mkdir -p $D
 C=multimodalpfn_amd/csrc
 T=/tmp/pipe_var_$name; mkdir -p $T
-sed -e "$script" $C/attention_pipe.hip > $T/attention_pipe.hip || exit 1
+sed -e "$script" ${SRC:-$C/attention_pipe.hip} > $T/attention_pipe.hip || exit 1
 cp $C/common.h $C/kernels.h $T/
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -mllvm -amdgpu-mfma-vgpr-form=1 \
   -fno-honor-nans $flags -x hip -c $T/attention_pipe.hip -o $T/attention_pipe.o || exit 1
