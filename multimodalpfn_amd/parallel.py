@@ -60,7 +60,9 @@ def allgather_logits(local: torch.Tensor, assignment: list[list[int]], rank: int
     tail = tuple(local.shape[1:])
     out = torch.empty((n_members,) + tail, device=local.device, dtype=local.dtype)
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
-        out[torch.as_tensor(assignment[rank], device=local.device, dtype=torch.long)] = local
+        if list(assignment[rank]) == list(range(n_members)):
+            return local  # one process running every member in order: nothing to move
+        out[_index(assignment[rank], local.device)] = local
         return out
     world = dist.get_world_size(group)
     assert len(assignment) == world and local.shape[0] == len(assignment[rank])
@@ -74,8 +76,17 @@ def allgather_logits(local: torch.Tensor, assignment: list[list[int]], rank: int
     gathered = gathered.to(local.device)
     for r, ids in enumerate(assignment):
         if ids:
-            out[torch.as_tensor(ids, device=local.device, dtype=torch.long)] = gathered[r * m_max : r * m_max + len(ids)]
+            out[_index(ids, local.device)] = gathered[r * m_max : r * m_max + len(ids)]
     return out
+
+
+def _index(ids, device) -> torch.Tensor:
+    """Member indices on the device without a host wait (pinned, non-blocking: a pageable copy would
+    block the host until the stream drains)."""
+    t = torch.as_tensor(list(ids), dtype=torch.long)
+    if device.type == "cuda":
+        return t.pin_memory().to(device, non_blocking=True)
+    return t.to(device)
 
 
 def member_shard(n_members: int, costs: list[float], group=None, keys: list | None = None, unit: int = 1):
