@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   }
   const int cnt = p.na + (g == p.kvb ? p.H * p.nb : 0);
   const int jw = chunk * P4_QPB + wave * P4_QPW;
-  const bool active = jw < cnt;  // wave-uniform; an idle wave still stages its share of every tile
+  const bool active = jw < cnt;  // wave-uniform; an idle wave only stages its share of every tile
 
   const int64_t kvoff = (int64_t)b * p.kv_bstride + (int64_t)g * p.Npad * 32;
   const bf16* Kg = p.k + kvoff;
@@ -333,6 +333,17 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     }
     gload(min(2, ntiles - 1), rk, rv);
     lds_barrier();
+    if (!active) {
+      // a wave without queries (a kv sequence's last, partial task) stages its share of every tile and
+      // meets every barrier, but issues none of the loop's MFMAs / exps: they would take issue slots
+      // from the other block's wave on its SIMD
+      for (int t = 0; t < nfull; ++t) {
+        lstore(ring + ((t + 2) & 3) * P4_SLOT_BYTES, rk, rv);
+        gload(min(t + 3, ntiles - 1), rk, rv);
+        lds_barrier();
+      }
+      return;  // no barrier follows the fast pass
+    }
     readk(kf[0], ring);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -378,6 +389,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     else pv(1, pz, vf[0]);
   }
 
+  if (!active) return;  // (nfull == 0: no barrier at all)
   // ---- one tile, not pipelined: the partial last tile of the fast pass, and every tile of the
   //      rare re-run with a reference (REF: s - mref; FIRST: mref = this tile's row max)
   float mref[P4_NCH] = {0.f, 0.f};
@@ -446,7 +458,6 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     }
   }
 
-  if (!active) return;
   // ---- row sums to the query's lanes, overflow backstop, normalise, store
 #pragma unroll
   for (int qb = 0; qb < P4_NCH; ++qb) {
