@@ -393,11 +393,16 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   // ---- one tile, not pipelined: the partial last tile of the fast pass, and every tile of the
   //      rare re-run with a reference (REF: s - mref; FIRST: mref = this tile's row max)
   float mref[P4_NCH] = {0.f, 0.f};
-  auto tile1 = [&](int t, bool first, bool ref) {
+  auto tile1 = [&](int t, bool first, bool ref, const unsigned char* slot) {
     const int k0 = t * P4_KT;
     bf16x8 kf[2][2], vf[2][2];
-    loadk(kf, t);
-    loadv(vf, t);
+    if (slot) {  // staged in the ring by the fast pass
+      readk(kf, slot);
+      readv(vf, slot);
+    } else {
+      loadk(kf, t);
+      loadv(vf, t);
+    }
     const bool mask = k0 + P4_KT > p.nk;
     if (mask) {  // keys >= nk: V = 0 so that p = 0 never meets NaN / inf padding
 #pragma unroll
@@ -435,7 +440,9 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       pv(qb, pb, vf);
     }
   };
-  if (partial) tile1(nfull, false, false);
+  // the partial last tile: staged by the fast pass into ring slot nfull % 4 (two tiles ahead, then left
+  // alone: the last iteration's clamped refill goes to slot (nfull + 1) % 4), behind that iteration's barrier
+  if (partial) tile1(nfull, false, false, nfull > 0 ? ring + (nfull & 3) * P4_SLOT_BYTES : nullptr);
 
   // the row sum of chain qb on the query's lanes (D rows 0 / 1 of lacc sit in lanes 0-15, registers 0 / 1)
   auto rowsum = [&](int qb) {
@@ -454,7 +461,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     }
     if (__any(bad)) {
       zero_acc();
-      for (int t = 0; t < ntiles; ++t) tile1(t, t == 0, true);
+      for (int t = 0; t < ntiles; ++t) tile1(t, t == 0, true, nullptr);
     }
   }
 
