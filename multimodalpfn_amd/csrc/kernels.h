@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "weight_pack.h"
+
 namespace mmpfn {
 
 // PREC_F32 (parity mode): every large contraction on bf16 MFMA with both operands split into
@@ -109,8 +111,7 @@ hipError_t launch_proj3_resln(const float* O, const void* W, int64_t w_lo, int64
 // table row, T <= 64 tokens; `pack` (capi.cpp pack_feat_rows) = LDS images with 416-B rows:
 // per head [96][FEAT_IMG_STRIDE] (Wq rows permuted & scaled by log2(e)/sqrt(32) | Wk rows
 // permuted | Wv), then the out-projection [192][FEAT_IMG_STRIDE] with permuted head columns
-constexpr int FEAT_IMG_STRIDE = 208;
-constexpr int FEAT_PACK_LAYER = (6 * 96 + 192) * FEAT_IMG_STRIDE;
+// (FEAT_IMG_STRIDE, FEAT_PACK_LAYER: weight_pack.h)
 // X holds M members [M][T][S][E]; one launch covers the M*S rows
 hipError_t launch_feat_rows(float* X, const void* pack, int S, int T, int M, int E, int H, float eps, hipStream_t st);
 
