@@ -476,8 +476,12 @@ class HipEngine:
     # ------------------------------------------------------------------ per-sublayer taps
     def _state_tap(self, X: torch.Tensor, fn, argf) -> torch.Tensor:
         """Run a C-ABI sublayer tap on a reference-order state ``[S, T, E]`` (copied to the
-        engine's token-major ``[T, S, E]``, updated in place, copied back)."""
-        Xt = self._dev(X).transpose(0, 1).contiguous()
+        engine's token-major ``[T, S, E]``, updated in place, copied back).  The working copy is always a
+        new tensor: with S == 1 or T == 1 the transposed view is already contiguous, and ``.contiguous()``
+        would hand the caller's own storage to the kernel."""
+        Xd = self._dev(X)
+        Xt = torch.empty((Xd.shape[1], Xd.shape[0]) + tuple(Xd.shape[2:]), dtype=Xd.dtype, device=Xd.device)
+        Xt.copy_(Xd.transpose(0, 1))
         T, S, _ = Xt.shape
         self._bind_stream()
         self._check(fn(self.ctx, *argf(Xt, S, T)), fn.__name__)

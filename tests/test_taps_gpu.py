@@ -99,3 +99,36 @@ def test_taps_at_config_c_shape(prec):
             err = rel_err(got.cpu().numpy(), ref.cpu().numpy())
             print(f"{name} prec {prec}: rel err {err:.2e}")
             assert err <= (TOL[1] if prec == 1 else 1e-4), (name, err)
+
+
+@pytest.mark.parametrize("prec", [1, 0])
+@pytest.mark.parametrize("S,T", [(1, 1), (5, 16), (130, 17), (7, 33), (66, 48), (3, 49), (129, 64), (9, 65)])
+def test_taps_ragged_shapes(S, T, prec):
+    """Shape edges of the layer kernels against the oracle (fp32 on the same GPU): token counts at and
+    past each 16-token tile of the feature block (T = 1 .. 64; T = 65 takes the general feature kernel),
+    row counts that leave a block's waves partly empty (S = 1, 3, 5, 7, 9, 66, 129, 130), one train row."""
+    from synth import synth_state_dict
+
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    torch.backends.cuda.matmul.allow_tf32 = False
+    cfg = ModelConfig(nlayers=1, mgm_heads=8, cap_heads=4)
+    sd = synth_state_dict(state_dict_spec(cfg), 3)
+    eng = _engine(cfg, sd)
+    spec, w = oracle_spec(cfg), {k: v.cuda() for k, v in torch_sd(sd).items()}
+    g = torch.Generator(device="cpu").manual_seed(S * 131 + T)
+    X = torch.randn(S, T, 192, generator=g).cuda()
+    X0 = X.clone()
+    N = max(1, (2 * S) // 3)
+    with torch.inference_mode():
+        for name, ref, got in [
+            ("feature", feat_sublayer(spec, w, 0, X), eng.feature_attention(0, X, prec)),
+            ("item", item_sublayer(spec, w, 0, X, N), eng.item_attention_block(0, X, N, prec)),
+            ("mlp", mlp_sublayer(spec, w, 0, X), eng.mlp_ln(0, X, prec)),
+        ]:
+            assert got.shape == ref.shape, name
+            assert torch.isfinite(got).all(), name
+            err = rel_err(got.cpu().numpy(), ref.cpu().numpy())
+            print(f"S={S} T={T} {name} prec {prec}: rel err {err:.2e}")
+            assert err <= (TOL[1] if prec == 1 else 1e-4), (name, err)
+    assert torch.equal(X, X0)  # the taps work on a copy (S = 1 or T = 1 once aliased the caller's state)
