@@ -150,6 +150,11 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   const int ntiles = (p.nk + P4_KT - 1) / P4_KT;
   const int nfull = p.nk / P4_KT;
   const bool partial = nfull != ntiles;
+  // key-tile order of the fast pass: the partial last tile first -- staged by the prologue with its keys
+  // >= nk zeroed (K rows 0: s = 0, p = 1 exactly; V^T 0: nothing added to O) -- then tiles 0 .. nfull-1,
+  // so every tile runs in the pipelined loop; each row sum then holds exactly npad extra ones
+  const int poff = partial ? 1 : 0;
+  auto tile_of = [&](int i) __attribute__((always_inline)) { return (partial && i == 0) ? nfull : i - poff; };
 
   // ---- fragments:
   //   K   A operand of S^T = K Q^T : lane (r, hh) <- K[key 32u + pk(r)][16ks + 8hh .. +7], pk swapping
@@ -194,6 +199,15 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   auto lstore = [&](unsigned char* slot, const u32x4& k, const u32x4& v) __attribute__((always_inline)) {
     *(u32x4*)(slot + kw) = k;
     *(u32x4*)(slot + vw) = v;
+  };
+  auto mask_pad = [&](u32x4& k, u32x4& v) {  // this thread's staging share of tile nfull, keys >= nk -> 0
+    const int k0 = nfull * P4_KT;
+    if (k0 + krow >= p.nk) k = u32x4{0u, 0u, 0u, 0u};
+    bf16x8 e = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (k0 + vc * 8 + j >= p.nk) e[j] = (bf16)0.0f;
+    v = __builtin_bit_cast(u32x4, e);
   };
   // one barrier per tile: the LDS writes done (lgkmcnt(0)), global loads left in flight
   auto lds_barrier = [&]() __attribute__((always_inline)) {
@@ -320,26 +334,27 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   //                writes tile t+2 (staged) to LDS, loads tile t+3 into the staging registers
   //   step (t, 1): S(t+1, chain 0) | exp S(t, chain 1) | P.V(t, chain 0); then the tile's barrier
   // kf(t) in register set t % 2, vf(t) in set (t + 1) % 2
-  if (nfull > 0) {
+  if (ntiles > 0) {
     bf16x8 kf[2][2][2], vf[2][2][2];
     f32x16 sa[2], sb[2];
     bf16x8 pa[2][2], pz[2][2];
     {  // tiles 0 and 1 in flight together, then tile 2 into the staging registers
       u32x4 rk1, rv1;
-      gload(0, rk, rv);
-      gload(min(1, ntiles - 1), rk1, rv1);
+      gload(tile_of(0), rk, rv);
+      gload(tile_of(min(1, ntiles - 1)), rk1, rv1);
+      if (partial) mask_pad(rk, rv);
       lstore(ring, rk, rv);
       lstore(ring + P4_SLOT_BYTES, rk1, rv1);
     }
-    gload(min(2, ntiles - 1), rk, rv);
+    gload(tile_of(min(2, ntiles - 1)), rk, rv);
     lds_barrier();
     if (!active) {
       // a wave without queries (a kv sequence's last, partial task) stages its share of every tile and
       // meets every barrier, but issues none of the loop's MFMAs / exps: they would take issue slots
       // from the other block's wave on its SIMD
-      for (int t = 0; t < nfull; ++t) {
+      for (int t = 0; t < ntiles; ++t) {
         lstore(ring + ((t + 2) & 3) * P4_SLOT_BYTES, rk, rv);
-        gload(min(t + 3, ntiles - 1), rk, rv);
+        gload(tile_of(min(t + 3, ntiles - 1)), rk, rv);
         lds_barrier();
       }
       return;  // no barrier follows the fast pass
@@ -359,7 +374,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       readk(kf[B], ring + S1);
       readv(vf[B], ring + S0);
       lstore(ring + S2, rk, rv);
-      gload(min(t + 3, ntiles - 1), rk, rv);
+      gload(tile_of(min(t + 3, ntiles - 1)), rk, rv);
       smm(sb, kf[A], 1);
       expc(pa, sa);
       pv(1, pz, vf[A]);
@@ -375,34 +390,29 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     using I2 = std::integral_constant<int, 2>;
     using I3 = std::integral_constant<int, 3>;
     int t = 0;
-    for (; t + 4 <= nfull; t += 4) {
+    for (; t + 4 <= ntiles; t += 4) {
       iter(I0{}, t);
       iter(I1{}, t + 1);
       iter(I2{}, t + 2);
       iter(I3{}, t + 3);
     }
-    if (t < nfull) iter(I0{}, t++);
-    if (t < nfull) iter(I1{}, t++);
-    if (t < nfull) iter(I2{}, t++);
-    // drain: P.V of the last full tile's chain 1 (vf(nfull - 1) sits in set nfull % 2)
-    if (nfull & 1) pv(1, pz, vf[1]);
+    if (t < ntiles) iter(I0{}, t++);
+    if (t < ntiles) iter(I1{}, t++);
+    if (t < ntiles) iter(I2{}, t++);
+    // drain: P.V of the last tile's chain 1 (vf(ntiles - 1) sits in set ntiles % 2)
+    if (ntiles & 1) pv(1, pz, vf[1]);
     else pv(1, pz, vf[0]);
   }
 
-  if (!active) return;  // (nfull == 0: no barrier at all)
-  // ---- one tile, not pipelined: the partial last tile of the fast pass, and every tile of the
-  //      rare re-run with a reference (REF: s - mref; FIRST: mref = this tile's row max)
+  if (!active) return;
+  // ---- one tile, not pipelined, straight from global memory: every tile of the rare re-run with a
+  //      reference (REF: s - mref; FIRST: mref = this tile's row max)
   float mref[P4_NCH] = {0.f, 0.f};
-  auto tile1 = [&](int t, bool first, bool ref, const unsigned char* slot) {
+  auto tile1 = [&](int t, bool first, bool ref) {
     const int k0 = t * P4_KT;
     bf16x8 kf[2][2], vf[2][2];
-    if (slot) {  // staged in the ring by the fast pass
-      readk(kf, slot);
-      readv(vf, slot);
-    } else {
-      loadk(kf, t);
-      loadv(vf, t);
-    }
+    loadk(kf, t);
+    loadv(vf, t);
     const bool mask = k0 + P4_KT > p.nk;
     if (mask) {  // keys >= nk: V = 0 so that p = 0 never meets NaN / inf padding
 #pragma unroll
@@ -440,9 +450,8 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       pv(qb, pb, vf);
     }
   };
-  // the partial last tile: staged by the fast pass into ring slot nfull % 4 (two tiles ahead, then left
-  // alone: the last iteration's clamped refill goes to slot (nfull + 1) % 4), behind that iteration's barrier
-  if (partial) tile1(nfull, false, false, nfull > 0 ? ring + (nfull & 3) * P4_SLOT_BYTES : nullptr);
+  // the fast pass's row sums include one p = 1 per padded key of the partial tile
+  float padsum = (float)(ntiles * P4_KT - p.nk);
 
   // the row sum of chain qb on the query's lanes (D rows 0 / 1 of lacc sit in lanes 0-15, registers 0 / 1)
   auto rowsum = [&](int qb) {
@@ -453,22 +462,25 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   };
   {  // reference-free pass out of [2^-60, 2^100) (tested on the bits; built with -fno-honor-nans) for
      // any query of the wave: re-run the wave with the first tile's row max
+    // (also when the padded keys' ones dominate a row sum: below 2^-10 of them the subtraction would cancel)
     bool bad = false;
 #pragma unroll
     for (int qb = 0; qb < P4_NCH; ++qb) {
-      const unsigned lb = __float_as_uint(rowsum(qb)) & 0x7fffffffu;
-      bad |= lb >= 0x71800000u || lb < 0x21800000u;
+      const float rs = rowsum(qb) - padsum;
+      const unsigned lb = __float_as_uint(rs) & 0x7fffffffu;
+      bad |= lb >= 0x71800000u || lb < 0x21800000u || rs < padsum * 0x1p-10f;
     }
     if (__any(bad)) {
       zero_acc();
-      for (int t = 0; t < ntiles; ++t) tile1(t, t == 0, true, nullptr);
+      for (int t = 0; t < ntiles; ++t) tile1(t, t == 0, true);
+      padsum = 0.f;  // the re-run masks the padded keys exactly
     }
   }
 
   // ---- row sums to the query's lanes, overflow backstop, normalise, store
 #pragma unroll
   for (int qb = 0; qb < P4_NCH; ++qb) {
-    const float ls = rowsum(qb);
+    const float ls = rowsum(qb) - padsum;
     const QRow q = qrow_of(qb);
     bf16* orow = p.o + ((int64_t)b * p.S + q.s) * (p.H * 32) + q.h * 32;
     if (__any((__float_as_uint(ls) & 0x7fffffffu) >= 0x71800000u)) {
