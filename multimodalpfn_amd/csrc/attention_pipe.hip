@@ -252,6 +252,11 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     }
   };
   zero_acc();
+  // the fast pass's row sums start at -npad: the partial tile (processed first) adds one p = 1 per padded
+  // key, so they cancel in its own MFMAs and every later tile accumulates at the scale of the true sum
+  const float padsum = (float)(ntiles * P4_KT - p.nk);
+#pragma unroll
+  for (int qb = 0; qb < P4_NCH; ++qb) lacc[qb] = f32x4{-padsum, -padsum, -padsum, -padsum};
 
   const f32x16 zero16 = {};
   auto smm = [&](f32x16(&s)[2], const bf16x8(&kf)[2][2], int qb) __attribute__((always_inline)) {
@@ -450,8 +455,6 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       pv(qb, pb, vf);
     }
   };
-  // the fast pass's row sums include one p = 1 per padded key of the partial tile
-  float padsum = (float)(ntiles * P4_KT - p.nk);
 
   // the row sum of chain qb on the query's lanes (D rows 0 / 1 of lacc sit in lanes 0-15, registers 0 / 1)
   auto rowsum = [&](int qb) {
@@ -462,25 +465,24 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   };
   {  // reference-free pass out of [2^-60, 2^100) (tested on the bits; built with -fno-honor-nans) for
      // any query of the wave: re-run the wave with the first tile's row max
-    // (also when the padded keys' ones dominate a row sum: below 2^-10 of them the subtraction would cancel)
+    // (also when a row sum is below 2^-12 npad: the cancelled ones left a few roundings at ulp(npad) in it)
     bool bad = false;
 #pragma unroll
     for (int qb = 0; qb < P4_NCH; ++qb) {
-      const float rs = rowsum(qb) - padsum;
+      const float rs = rowsum(qb);
       const unsigned lb = __float_as_uint(rs) & 0x7fffffffu;
-      bad |= lb >= 0x71800000u || lb < 0x21800000u || rs < padsum * 0x1p-10f;
+      bad |= lb >= 0x71800000u || lb < 0x21800000u || rs < padsum * 0x1p-12f;
     }
     if (__any(bad)) {
       zero_acc();
       for (int t = 0; t < ntiles; ++t) tile1(t, t == 0, true);
-      padsum = 0.f;  // the re-run masks the padded keys exactly
     }
   }
 
   // ---- row sums to the query's lanes, overflow backstop, normalise, store
 #pragma unroll
   for (int qb = 0; qb < P4_NCH; ++qb) {
-    const float ls = rowsum(qb) - padsum;
+    const float ls = rowsum(qb);
     const QRow q = qrow_of(qb);
     bf16* orow = p.o + ((int64_t)b * p.S + q.s) * (p.H * 32) + q.h * 32;
     if (__any((__float_as_uint(ls) & 0x7fffffffu) >= 0x71800000u)) {
