@@ -276,6 +276,24 @@ def test_item_attention_reference_rerun(kscale, prec):
     assert err < (2e-2 if prec == 1 else 1e-4)
 
 
+@pytest.mark.parametrize("N", [65, 1838])
+@pytest.mark.parametrize("kscale", [-0.6, -0.7, -0.8, -0.9])
+def test_item_attention_padded_tile_small_sums(kscale, N):
+    """The partial key tile runs in the pipelined loop with its padded keys at p = 1 and the row sums
+    started at -npad (63 or 18 padded keys here); scores of about 16 kscale log2 units put the true sums
+    around 2^-12 npad, on both sides of the threshold below which the wave takes the exact re-run."""
+    S, T = N + 40, 1
+    q, k, v, Npad = _qkv_case(S, N, T, seed=N + 3)
+    q[...] = q.sign() * 0.1 + 2.0
+    k[...] = k * 0.02 + kscale
+    got = _launch_layer(q, k, v, Npad, N, 1)
+    ref = _layer_ref(q, k, v, N, 1)
+    assert torch.isfinite(got).all()
+    err = (got.double() - ref).abs().max().item()
+    print(f"padded tile N={N} kscale {kscale}: {err:.3e}")
+    assert err < 2e-2
+
+
 def test_engine_deterministic_and_no_nan_at_pad_ufes_size():
     """Full config-C geometry (N=1838, Q=460, F=21, mgm 64 / cap 24): run twice, bitwise equal;
     bf16 vs fp32 engine argmax agreement (size-independent properties)."""
