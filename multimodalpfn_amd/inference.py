@@ -19,6 +19,7 @@ across ranks (longest-processing-time) and the logits all-gathered (RCCL).
 
 from __future__ import annotations
 
+
 from collections.abc import Iterator, Sequence
 from dataclasses import dataclass, field
 from typing import Any, Literal
@@ -124,26 +125,19 @@ class InferenceEngine:
         tokens = _mixer_tokens(model, eng, image_train, image_test, prec, cache) if mine else None
         # launch order: geometry groups (members the engine stacks into one batched forward) narrowest
         # first, so the GPU starts after the cheapest transforms and the wider members' transforms run
-        # under the earlier units' forwards.  The transforms run in that order on ONE worker thread:
-        # sklearn's per-call Python overhead holds the GIL, so parallel workers only finish every member
-        # later (measured on the host: four workers finish all four members together, at about the serial sum)
+        # under the earlier units' forwards.  Each member is transformed in the main thread when its unit
+        # is assembled: a worker thread (tried with one and with four) holds the GIL for sklearn's per-call
+        # overhead exactly while the main thread enqueues the previous unit's kernels, and measured 2-3 ms
+        # slower per predict at config C (19.1 / 17.5 vs 16.1 / 15.6 ms; default preprocessing 19.7 / 20.1 vs
+        # 17.8 / 17.4 ms, profiles/r03/ab/api_transform_inline.txt)
         order = self._launch_order(members, mine)
-        pending = {}
-        pool = None
-        todo = [i for i in order if members[i].X_train is not None]
-        if len(todo) > 1:
-            from concurrent.futures import ThreadPoolExecutor
-
-            pool = ThreadPoolExecutor(max_workers=1)
-            pending = {i: pool.submit(lambda p=members[i].preprocessor: p.transform(X).X) for i in todo}
 
         def items():  # a generator: forward_many launches each unit as soon as its members are ready
             for i in order:
                 m = members[i]
                 x_full = None
                 if m.X_train is not None:
-                    xt = pending[i].result() if i in pending else m.preprocessor.transform(X).X
-                    X_test = _h2d(xt, eng.device)
+                    X_test = _h2d(m.preprocessor.transform(X).X, eng.device)
                     key = ("X_train", i, str(eng.device))
                     xtr = None if cache is None else cache.get(key)
                     if xtr is None:
@@ -153,13 +147,7 @@ class InferenceEngine:
                     x_full = torch.cat([xtr, X_test], 0)
                 yield x_full, tokens, np.asarray(m.y_train, np.float32)
 
-        try:
-            outs: dict[int, torch.Tensor] = dict(zip(order, eng.forward_many(items(), prec)))
-        finally:
-            if pool is not None:
-                for f in pending.values():
-                    f.cancel()
-                pool.shutdown(wait=True)
+        outs: dict[int, torch.Tensor] = dict(zip(order, eng.forward_many(items(), prec)))
         if mine:
             eng.status()  # NaN / HIP errors of every queued member (transformer.py:727-731,790-796)
         Q = len(X) if X is not None else len(image_test)
