@@ -25,6 +25,9 @@
  *   mmpfn_item_attention_layer
  *       <- model/layer.py:341-379 attn_between_items of one layer: train rows
  *          (:362-372) and test rows against head 0's K/V (:344-358) together
+ *   mmpfn_item_attention_cached
+ *       <- model/layer.py:344-358 with multi_head_attention.py:461-472: test rows of
+ *          every head against the cached head-0 K/V of the train rows (fit_with_cache)
  *   mmpfn_status
  *       <- model/transformer.py:727-731,790-796 NaN checks (ValueError)
  *   mmpfn_feature_attention / mmpfn_item_attention_block / mmpfn_mlp_ln
@@ -160,6 +163,12 @@ int mmpfn_select_lane(mmpfn_ctx* ctx, int lane);
  * K/V head 0; keys [0, N).  Layouts as mmpfn_item_attention. */
 int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
                                int T, int H, int Npad, int N);
+
+/* The train-KV cache's attention (bf16 only): queries s in [0, S) of every head against a
+ * head-0-only K [T][Npad][32] / V^T [T][32][Npad] (the layout mmpfn_cache_build keeps per
+ * layer); keys [0, N).  Q / out as mmpfn_item_attention. */
+int mmpfn_item_attention_cached(mmpfn_ctx* ctx, const void* q, const void* k0, const void* vt0, void* out, int S,
+                                int T, int H, int Npad, int N);
 
 /* Train-KV cache (fit_mode="fit_with_cache"), one per ensemble member.
  * mmpfn_cache_build: forward of the N train rows only (x [N][F], tokens [N][C][E], y_train [N]);

@@ -1208,6 +1208,16 @@ int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, con
   return MMPFN_OK;
 }
 
+int mmpfn_item_attention_cached(mmpfn_ctx* ctx, const void* q, const void* k0, const void* vt0, void* out, int S,
+                                int T, int H, int Npad, int N) {
+  if (!ctx || !q || !k0 || !vt0 || !out) return MMPFN_ERR_INVALID;
+  if (S <= 0 || N <= 0 || N > Npad || Npad % 64 || H <= 0 || H > 8 || T <= 0)
+    return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(launch_attn_layer(q, k0, vt0, out, S, T, H, Npad, N, 0, 0, 0, S, 0, ctx->stream, (int64_t)Npad * 32));
+  return MMPFN_OK;
+}
+
 // ---- per-sublayer taps ------------------------------------------------------------
 static int tap_check(mmpfn_ctx* ctx, int layer, const void* X, int precision) {
   if (!ctx || !X) return MMPFN_ERR_INVALID;

@@ -14,7 +14,23 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 namespace mmpfn {
+
+// Opt-in of a kernel to more than 64 KiB of dynamic LDS.  HIP keeps the attribute per device, so it
+// is set once per device that launches the kernel (`opted`: one bit per device, owned by the call
+// site) and a failure is returned, never remembered.
+inline hipError_t lds_optin(std::atomic<uint64_t>& opted, const void* fn, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const uint64_t bit = dev < 64 ? (uint64_t)1 << dev : 0;
+  if (bit && (opted.load(std::memory_order_relaxed) & bit)) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) opted.fetch_or(bit, std::memory_order_relaxed);
+  return e;
+}
 
 typedef __bf16 bf16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;

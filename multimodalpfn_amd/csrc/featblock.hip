@@ -405,13 +405,9 @@ hipError_t launch_feat_block(float* X, const void* wqkv, const void* wout, int S
   a.X = X, a.wqkv = (const bf16*)wqkv, a.wout = (const bf16*)wout;
   a.S = S, a.T = T, a.R = R, a.Mp = (R * T + 15) / 16 * 16;
   a.eps = eps, a.qscale = kLog2e * 0.17677669529663687f;  // log2(e) / sqrt(32)
-  static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)feat_block_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)feat_block_lds(MAXTOK));
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> opted{0};  // > 64 KiB dynamic LDS needs an explicit opt-in
+  const hipError_t e = lds_optin(opted, (const void*)feat_block_kernel, (int)feat_block_lds(MAXTOK));
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(feat_block_kernel, dim3((S + R - 1) / R), dim3(256), feat_block_lds(a.Mp), st, a);
   return hipGetLastError();
 }

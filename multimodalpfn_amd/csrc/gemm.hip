@@ -381,9 +381,9 @@ hipError_t launch_t(const GemmArgs& a, int groups, hipStream_t st) {
   constexpr int STAGE = MODE == 2 ? LDS_STAGE_X3 : LDS_STAGE;
   const int lds = STAGED > STAGE ? STAGED : STAGE;
   if (lds > 65536) {  // x3: 80 KB of hi / lo planes
-    static const hipError_t attr = hipFuncSetAttribute((const void*)gemm_kernel<MODE, AF32, OF32, EPI>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (attr != hipSuccess) return attr;
+    static std::atomic<uint64_t> opted{0};
+    const hipError_t e = lds_optin(opted, (const void*)gemm_kernel<MODE, AF32, OF32, EPI>, lds);
+    if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL((gemm_kernel<MODE, AF32, OF32, EPI>), grid, dim3(256), lds, st, a);
   return hipGetLastError();

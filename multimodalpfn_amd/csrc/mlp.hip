@@ -369,16 +369,11 @@ hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M,
   if (M <= 0) return hipSuccess;
   if (E != ME || Fh % ME != 0) return hipErrorInvalidValue;
   dim3 grid((M + MBM - 1) / MBM);
-  static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)mlp_fused_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       MlpLds<1>::BYTES);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)mlp_fused_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            MlpLds<0>::BYTES);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> opted1{0}, opted0{0};  // > 64 KiB dynamic LDS needs an explicit opt-in
+  hipError_t e = lds_optin(opted1, (const void*)mlp_fused_kernel<1>, MlpLds<1>::BYTES);
+  if (e != hipSuccess) return e;
+  e = lds_optin(opted0, (const void*)mlp_fused_kernel<0>, MlpLds<0>::BYTES);
+  if (e != hipSuccess) return e;
   if (prec == PREC_BF16)
     hipLaunchKernelGGL(mlp_fused_kernel<1>, grid, dim3(256), MlpLds<1>::BYTES, st, X, W1, W2, (int)M, Fh, eps);
   else if (prec == PREC_F32)  // W1 natural, W2 in the pack_mlp2_perm order, each as hi | lo planes

@@ -268,8 +268,8 @@ int n_cus() {
 
 template <bool RESLN>
 hipError_t launch_p3(const P3Args& a, hipStream_t st) {
-  static const hipError_t attr =
-      hipFuncSetAttribute((const void*)proj3_kernel<RESLN>, hipFuncAttributeMaxDynamicSharedMemorySize, P3LDS);
+  static std::atomic<uint64_t> opted{0};
+  const hipError_t attr = lds_optin(opted, (const void*)proj3_kernel<RESLN>, P3LDS);
   if (attr != hipSuccess) return attr;
   const int grid = std::min(n_cus(), (a.total + P3W - 1) / P3W);
   hipLaunchKernelGGL(proj3_kernel<RESLN>, dim3(grid), dim3(64 * P3W), P3LDS, st, a);

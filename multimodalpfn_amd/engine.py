@@ -14,6 +14,7 @@ shapes and the few host-side constants the reference also computes on the host:
 from __future__ import annotations
 
 import ctypes
+import itertools
 import os
 
 import numpy as np
@@ -79,6 +80,7 @@ DEFAULT_BATCH = int(os.environ.get("MMPFN_BATCH", "2"))  # members per batched f
 _DEBUG_SYNC = os.environ.get("MMPFN_DEBUG_SYNC") == "1"  # diagnostics: serialise forward_many's units
 _DEBUG_KEEP = os.environ.get("MMPFN_DEBUG_KEEP") == "1"  # diagnostics: keep every prepared input alive
 _KEEP: list = []
+_SERIAL = itertools.count(1)  # engine serial numbers: cache tags that a freed engine's id() could alias
 
 
 class HipEngine:
@@ -118,6 +120,7 @@ class HipEngine:
         self.lanes = DEFAULT_LANES
         self.batch = DEFAULT_BATCH
         self.refs = 1  # model copies holding this engine (PerFeatureTransformer.__deepcopy__ shares it)
+        self.serial = next(_SERIAL)
 
     # ------------------------------------------------------------------ plumbing
     def _stream(self) -> int:

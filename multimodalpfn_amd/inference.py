@@ -118,7 +118,7 @@ class InferenceEngine:
         if cache is not None:
             # device copies made with other weights (load_state_dict / invalidate_engine after fit) or by
             # another engine are stale
-            tag = (model._weights_version, id(eng))
+            tag = (model._weights_version, eng.serial)
             if cache.get("_tag") != tag:
                 cache.clear()
                 cache["_tag"] = tag
@@ -282,7 +282,7 @@ class InferenceEngineCacheKV(InferenceEngine):
     @classmethod
     def prepare(cls, X_train, y_train, image_train, *, cat_ix, model, ensemble_configs, n_workers, rng,
                 dtype_byte_size, force_inference_dtype, save_peak_mem, device, autocast) -> InferenceEngineCacheKV:
-        from multimodalpfn_amd.parallel import member_shard
+        from multimodalpfn_amd.parallel import member_cost, member_shard
 
         itr = fit_preprocessing(configs=ensemble_configs, X_train=X_train, y_train=y_train, random_state=rng,
                                 cat_ix=cat_ix, n_workers=n_workers, parallel_mode="block")
@@ -290,7 +290,15 @@ class InferenceEngineCacheKV(InferenceEngine):
         model = model.to(device)
         eng = model.engine(device)
         prec = _precision(model, eng.device, autocast, force_inference_dtype)
-        costs = [float(len(y)) ** 2 for y in y_trains]
+        # the flop model of the other engines (parallel.member_cost) on each member's cache build:
+        # T tokens of N train rows against N keys (ragged widths make T differ between members)
+        C = _n_mixer_tokens(model, image_train)
+        fpg = model.features_per_group
+        costs = []
+        for xt, yt in zip(X_trains, y_trains):
+            F = 0 if xt is None else np.asarray(xt).shape[1]
+            costs.append(member_cost((F + fpg - 1) // fpg + C + 1, len(yt), len(yt), model.cfg.emsize,
+                                     model.cfg.nhid))
         mine, gather = member_shard(len(configs), costs)
         tokens = None
         if image_train is not None and model.mixer_type in ("MGM", "MGM+CAP", "MoE") and mine:

@@ -47,19 +47,23 @@ def member_cost(n_tokens: int, S: int, N: int, E: int = 192, FF: int = 768) -> f
     return T * S * E * (16.0 * E + 4.0 * FF + 4.0 * N + 4.0 * T)
 
 
-def allgather_logits(local: torch.Tensor, assignment: list[list[int]], rank: int, group=None) -> torch.Tensor:
+def allgather_logits(local: torch.Tensor, assignment: list[list[int]], rank: int, group=None,
+                     force_collective: bool = False) -> torch.Tensor:
     """Gather every rank's ``[m_r, Q, n_out]`` logits into ``[n_members, Q, n_out]`` in member order.
 
     ``assignment`` (identical on every rank, from :func:`lpt_assign`) fixes the block
     sizes, so this is exactly one fixed-size ``all_gather`` of ``max_r m_r`` padded
-    blocks; with one process it is a reorder.
+    blocks; with one process it is a reorder.  ``force_collective`` (tests) takes the
+    collective branch even for a world of one, so a single-GPU box executes the RCCL
+    all-gather path.
     """
     import torch.distributed as dist
 
     n_members = sum(len(a) for a in assignment)
     tail = tuple(local.shape[1:])
     out = torch.empty((n_members,) + tail, device=local.device, dtype=local.dtype)
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+    distributed = dist.is_available() and dist.is_initialized()
+    if not distributed or (dist.get_world_size(group) == 1 and not force_collective):
         if list(assignment[rank]) == list(range(n_members)):
             return local  # one process running every member in order: nothing to move
         out[_index(assignment[rank], local.device)] = local

@@ -13,6 +13,8 @@ import numpy as np
 import pytest
 import torch
 
+from helpers import check_argmax
+
 from test_api_host import HERE, NAMES, _case, case_data, make_classifier, write_ckpt
 
 pytestmark = pytest.mark.gpu
@@ -60,9 +62,10 @@ def test_predict_proba_bf16_close(name, tmp_path):
     clf.fit(d["X_train"], d["image_train"], d["y_train"])
     assert clf.use_autocast_
     proba = clf.predict_proba(d["X_test"], d["image_test"])
-    assert np.abs(proba - z["proba"]).max() < 5e-2
-    agree = (proba.argmax(1) == z["proba"].argmax(1)).mean()
-    assert agree >= 0.9, agree
+    err = np.abs(proba - z["proba"]).max()
+    print(f"{name}: bf16 proba max |err| {err:.3e}")
+    assert err < 3e-2, err
+    check_argmax(proba, z["proba"], 0.995, f"api {name} bf16")
 
 
 def test_low_memory_mode_is_reproducible(tmp_path):

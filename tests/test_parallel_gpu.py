@@ -87,3 +87,43 @@ def test_sharded_predict_proba_equals_single_process(tmp_path):
     assert len(by_rank[0]) == len(by_rank[1]) >= 2
     for (n0, m0), (n1, m1) in zip(by_rank[0], by_rank[1]):
         assert n0 == n1 and m0 and m1 and sorted(m0 + m1) == list(range(n0)), (m0, m1)
+
+
+def _nccl_world1(port, q):
+    """A fresh process: RCCL process group of one rank, then the all-gather's collective branch."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    try:
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        torch.cuda.set_device(0)
+        from multimodalpfn_amd.parallel import allgather_logits
+
+        g = torch.Generator().manual_seed(7)
+        local = torch.randn((5, 460, 10), generator=g).cuda()
+        assignment = [[3, 0, 4, 1, 2]]  # a non-identity member order: the reorder is exercised too
+        coll = allgather_logits(local, assignment, 0, force_collective=True)
+        ref = allgather_logits(local, assignment, 0)
+        torch.cuda.synchronize()
+        q.put((dist.get_backend(), coll.device.type, bool(torch.equal(coll, ref)),
+               bool(torch.equal(ref[torch.tensor(assignment[0])], local)), None))
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        q.put((None, None, False, False, f"{type(e).__name__}: {e}"))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_rccl_allgather_branch_world1():
+    """the device-tensor ``all_gather_into_tensor`` of ``allgather_logits`` runs on RCCL
+    (backend ``nccl``) with one rank, forced past the world-size-1 short-circuit, and equals the reorder path
+    bitwise (parallel.py; the reference's member mean, classifier.py:555-561, has no collective)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_world1, args=(_free_port(), q))
+    p.start()
+    backend, dev, equal, reordered, err = q.get(timeout=180)
+    p.join(timeout=60)
+    assert err is None, err
+    assert backend == "nccl" and dev == "cuda"
+    assert equal and reordered
