@@ -56,6 +56,10 @@ extern "C" {
                                   bf16 hi + lo planes (hi.hi + hi.lo + lo.hi, fp32 accumulate: ~2^-16 relative) */
 #define MMPFN_PREC_BF16 1     /* performance mode: bf16 MFMA operands, fp32 accumulate / residual / LN */
 #define MMPFN_PREC_F32_MFMA 2 /* parity mode on fp32-input MFMA (exact fp32 fma chains, 1/16 of the bf16 rate) */
+#define MMPFN_PREC_BF16_F8 3  /* MMPFN_PREC_BF16 with the sample-axis attention's P.V and row sums on block-scaled fp8
+                                  MFMA (V^T e4m3, P e4m3 under a per-query power-of-two scale): config E's fp8 path
+                                  (multi_head_attention.py:693-729 in fp8); the train-KV cache keeps bf16 */
+#define MMPFN_PREC_BF16_F8E5 4 /* as MMPFN_PREC_BF16_F8 with P in e5m2 (wider range, 2 mantissa bits) */
 
 #define MMPFN_MIXER_NONE 0
 #define MMPFN_MIXER_MGM 1
@@ -163,6 +167,11 @@ int mmpfn_select_lane(mmpfn_ctx* ctx, int lane);
  * K/V head 0; keys [0, N).  Layouts as mmpfn_item_attention. */
 int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
                                int T, int H, int Npad, int N);
+
+/* mmpfn_item_attention_layer with the fp8 P.V of MMPFN_PREC_BF16_F8 (p_format 1: P e4m3) or
+ * MMPFN_PREC_BF16_F8E5 (p_format 2: P e5m2); vt is the bf16 V^T (converted to e4m3 inside). */
+int mmpfn_item_attention_layer_fp8(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
+                                   int T, int H, int Npad, int N, int p_format);
 
 /* The train-KV cache's attention (bf16 only): queries s in [0, S) of every head against a
  * head-0-only K [T][Npad][32] / V^T [T][32][Npad] (the layout mmpfn_cache_build keeps per

@@ -24,11 +24,28 @@ MMPFN_ERR_WEIGHT = -5
 PREC_F32 = 0       # parity mode: split-bf16 three-product MFMAs (fp32 operands to 2^-16), fp32 softmax / LN
 PREC_BF16 = 1      # performance mode (the reference's fp16 autocast counterpart)
 PREC_F32_MFMA = 2  # parity mode on fp32-input MFMA (exact fp32 fma chains, 1/16 of the bf16 rate)
+PREC_BF16_F8 = 3   # bf16 mode with the sample-axis attention's P.V on fp8 MFMA (P e4m3): config E's fp8 path
+PREC_BF16_F8E5 = 4  # the same with P in e5m2
 
 
 def f32_precision() -> int:
     """Engine code of an fp32 forward: PREC_F32, or PREC_F32_MFMA under ``MMPFN_F32_MODE=mfma``."""
     return PREC_F32_MFMA if os.environ.get("MMPFN_F32_MODE", "").lower() == "mfma" else PREC_F32
+
+
+def precision_of_dtype(dtype) -> int:
+    """Engine code of a forced ``inference_precision`` dtype (the reference's ``force_inference_dtype``):
+    fp32 / fp64 -> the parity mode; ``torch.float8_e4m3fn`` / ``torch.float8_e5m2`` -> the 16-bit mode with
+    the attention's P.V on fp8 MFMA (P in that format); any other dtype -> the 16-bit performance mode."""
+    import torch
+
+    if dtype in (torch.float32, torch.float64):
+        return f32_precision()
+    if dtype == torch.float8_e4m3fn:
+        return PREC_BF16_F8
+    if dtype == torch.float8_e5m2:
+        return PREC_BF16_F8E5
+    return PREC_BF16
 
 MIXER_NONE, MIXER_MGM, MIXER_MGM_CAP, MIXER_MOE = 0, 1, 2, 3
 MIXER_CODES = {"MGM": MIXER_MGM, "MGM+CAP": MIXER_MGM_CAP, "MoE": MIXER_MOE, None: MIXER_NONE}
@@ -77,6 +94,7 @@ SIGNATURES = [
     ("mmpfn_item_attention", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i]),
     ("mmpfn_item_attention_layer", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i]),
     ("mmpfn_item_attention_cached", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i]),
+    ("mmpfn_item_attention_layer_fp8", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i]),
     ("mmpfn_select_lane", _i, [_vp, _i]),
     ("mmpfn_forward_batch", _i, [_vp, _i, _vp, _i, _i, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _i]),
     ("mmpfn_cache_build", _i, [_vp, _vp, _i, _i, _vp, _i, _vp, _vp, _i, _vp, _i, ctypes.POINTER(_vp)]),

@@ -830,7 +830,8 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
 namespace {
 hipError_t launch_item_attention(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
                                  int Npad, int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st,
-                                 int64_t kv_bstride, bool q_prescaled, bool x3) {
+                                 int64_t kv_bstride, bool q_prescaled, bool x3, const void* vt8 = nullptr,
+                                 int f8 = 0) {
   if (na + nb <= 0 || T <= 0) return hipSuccess;
   if (nk <= 0 || Npad % A2_KT != 0 || nk > Npad || H > 8 || H <= 0) return hipErrorInvalidValue;
   if (nb > 0 && (kvb < 0 || kvb >= H)) return hipErrorInvalidValue;
@@ -840,6 +841,7 @@ hipError_t launch_item_attention(const void* q, const void* k, const void* vt, v
   a.a0 = a0, a.na = na, a.b0 = b0, a.nb = nb, a.kvb = nb > 0 ? kvb : -1;
   a.kv_bstride = kv_bstride > 0 ? kv_bstride : (int64_t)H * Npad * 32;
   a.q_prescaled = q_prescaled ? 1 : 0;
+  a.vt8 = (const unsigned char*)vt8, a.f8 = x3 ? 0 : f8;
   if (kv_bstride > 0 && (na > 0 || kvb != 0)) return hipErrorInvalidValue;  // cache layout holds head 0 only
   const int qpb = x3 ? A3_QPB : ATTN_ITEM_QPB;
   int acc = 0;
@@ -863,9 +865,9 @@ hipError_t launch_item_attention(const void* q, const void* k, const void* vt, v
 
 hipError_t launch_attn_layer(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride,
-                             bool q_prescaled) {
+                             bool q_prescaled, const void* vt8, int f8) {
   return launch_item_attention(q, k, vt, out, S, T, H, Npad, nk, a0, na, b0, nb, kvb, st, kv_bstride, q_prescaled,
-                               false);
+                               false, vt8, f8);
 }
 
 hipError_t launch_attn_item3(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,

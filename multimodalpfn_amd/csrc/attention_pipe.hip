@@ -21,6 +21,16 @@
 // Softmax: fixed reference 0 (Q carries log2(e)/sqrt(32)), p = exp2(s), row
 // sums on the MFMA pipe through a 0/1 selector, the sum range-checked per wave ([2^-60, 2^100)),
 // a wave out of range re-running with the first tile's row max, and an exact two-pass backstop.
+//
+// F8 variants (config E's "fp8 MFMA path", BASELINE.json configs[4]; opt-in): P.V and the row sums on the
+// block-scaled v_mfma_scale_f32_32x32x64_f8f6f4 / _16x16x128_ (one MFMA each per chain and 64-key tile
+// instead of 4 + 4: 12 instead of 24 MFMA issue holds per tile-wave), V^T in e4m3 (converted once after
+// the projection, launch_vt_fp8), P in e4m3 (F8 = 1) or e5m2 (F8 = 2).  S = K Q^T stays bf16.  fp8 has no
+// room for the fixed reference 0, so each query gets a power-of-two conversion scale from its first key
+// tile's max (the first tile's max lands at 2^ETOP); a later score beyond the format's range converts to
+// NaN / inf, which the row-sum check catches, and the wave re-runs on the exact bf16 path.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -35,6 +45,26 @@ constexpr int P4_QPB = 4 * P4_QPW;
 static_assert(P4_QPB == ATTN_ITEM_QPB, "launch_item_attention's task size");
 
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(2))) short s16x2;
+
+// fp8 P formats: conversion, MFMA operand format code, where the first tile's max lands (2^ETOP) and the
+// smallest power of two the format still holds (subnormal)
+template <int F8> struct P8;
+template <> struct P8<1> {  // e4m3 (max 448 = 2^8.8): >= 5.8 octaves of headroom, 11 below the first max
+  static constexpr int FMT = 0, ETOP = 2, EMIN = -9, EMAX = 8;
+  static __device__ __forceinline__ s16x2 cvt(s16x2 old, float a, float b, float sc, bool hi) {
+    return hi ? __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(old, a, b, sc, true)
+              : __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(old, a, b, sc, false);
+  }
+};
+template <> struct P8<2> {  // e5m2 (max 57344 = 2^15.8): >= 8.8 octaves of headroom, 22 below
+  static constexpr int FMT = 1, ETOP = 6, EMIN = -16, EMAX = 15;
+  static __device__ __forceinline__ s16x2 cvt(s16x2 old, float a, float b, float sc, bool hi) {
+    return hi ? __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(old, a, b, sc, true)
+              : __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(old, a, b, sc, false);
+  }
+};
 
 // sched_group_barrier masks (LLVM AMDGPU IGroupLP)
 constexpr int SG_VALU = 0x2, SG_MFMA = 0x8, SG_VMEM_READ = 0x20, SG_DS_READ = 0x100, SG_DS_WRITE = 0x200,
@@ -77,10 +107,11 @@ __device__ __attribute__((noinline)) void p4_exact_rows(const Attn2Args& p, cons
   }
 }
 
-#ifndef P4_SLOT_BYTES
-#define P4_SLOT_BYTES (64 * 80 + 32 * 144)
-#endif
+template <int F8>
 __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
+  // LDS slot: K [64][32] bf16 in 80-B rows | V^T [32][64] in 144-B rows (bf16) or 80-B rows (e4m3)
+  constexpr int VROW = F8 ? 80 : 144;
+  constexpr int P4_SLOT_BYTES = 64 * 80 + 32 * VROW;
   __shared__ __attribute__((aligned(16))) unsigned char ring[4 * P4_SLOT_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -110,6 +141,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   const int64_t kvoff = (int64_t)b * p.kv_bstride + (int64_t)g * p.Npad * 32;
   const bf16* Kg = p.k + kvoff;
   const bf16* Vg = p.vt + kvoff;
+  const unsigned char* Vg8 = p.vt8 + kvoff;  // F8: e4m3 V^T, same element layout
   const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
 
   // the lane's query of chain qb: head and table row (recomputed after the tile loop rather than kept live)
@@ -165,8 +197,11 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   // LDS ring: slot = K [64][32] in 80-B rows | V^T [32][64] in 144-B rows: the padded strides make the
   // ds_read_b128 of every 16-lane group conflict-free (row * 20 and d * 36 dwords are distinct mod 64
   // over 16 rows), and every fragment of a lane sits at one base + an immediate offset
-  constexpr int KROW = 80, VROW = 144, VBASE = 64 * KROW;
-  const int kb = (32 * 0 + pkr) * KROW + 16 * hh, vb = VBASE + r * VROW + 16 * hh;
+  //   F8: V^T A operand of the 32x32x64 MFMA: lane (r = d, hh) <- V^T[d][logical k 32hh .. 32hh+31], logical
+  //       k 32hh + 8j + b = key 16j + 8hh + b (the keys of the P bytes, see expc): an e4m3 V^T row is stored
+  //       with key group g (8 keys) at byte 32 (g & 1) + 8 (g >> 1), so a lane reads 32 contiguous bytes
+  constexpr int KROW = 80, VBASE = 64 * KROW;
+  const int kb = (32 * 0 + pkr) * KROW + 16 * hh, vb = VBASE + r * VROW + (F8 ? 32 : 16) * hh;
   int kro[2][2], vro[2][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -181,33 +216,52 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) kf[u][ks] = *(const bf16x8*)(slot + kro[u][ks]);
   };
-  auto readv = [&](bf16x8(&vf)[2][2], const unsigned char* slot) __attribute__((always_inline)) {
+  using VFrag = std::conditional_t<F8 != 0, i32x8, bf16x8[2][2]>;  // V^T fragments of one tile
+  using PFrag = std::conditional_t<F8 != 0, i32x8, bf16x8[2][2]>;  // P^T fragments of one (tile, chain)
+  using VStage = std::conditional_t<F8 != 0, u32x2, u32x4>;        // a thread's V^T staging share
+  auto readv = [&](VFrag& vf, const unsigned char* slot) __attribute__((always_inline)) {
+    if constexpr (F8 != 0) {
+      const u32x4 a = *(const u32x4*)(slot + vb), c = *(const u32x4*)(slot + vb + 16);
+      vf = i32x8{(int)a.x, (int)a.y, (int)a.z, (int)a.w, (int)c.x, (int)c.y, (int)c.z, (int)c.w};
+    } else {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int sp = 0; sp < 2; ++sp) vf[u][sp] = *(const bf16x8*)(slot + vro[u][sp]);
+        for (int sp = 0; sp < 2; ++sp) vf[u][sp] = *(const bf16x8*)(slot + vro[u][sp]);
+    }
   };
-  // staging: thread tid holds K row tid >> 2 chunk tid & 3 and V^T row tid >> 3 chunk tid & 7 of a tile
+  // staging: thread tid holds K row tid >> 2 chunk tid & 3 and V^T row tid >> 3 key group tid & 7 of a tile
   const int krow = tid >> 2, kc = tid & 3, vd = tid >> 3, vc = tid & 7;
   const int kso = krow * 32 + kc * 8, vso = vd * p.Npad + vc * 8;  // 32-bit lane offsets on wave-uniform bases
-  const int kw = krow * KROW + 16 * kc, vw = VBASE + vd * VROW + 16 * vc;
-  u32x4 rk, rv;
-  auto gload = [&](int t, u32x4& k, u32x4& v) __attribute__((always_inline)) {
+  const int kw = krow * KROW + 16 * kc;
+  const int vw = F8 ? VBASE + vd * VROW + 32 * (vc & 1) + 8 * (vc >> 1) : VBASE + vd * VROW + 16 * vc;
+  u32x4 rk;
+  VStage rv;
+  auto gload = [&](int t, u32x4& k, VStage& v) __attribute__((always_inline)) {
     k = *(const u32x4*)(Kg + (int64_t)t * (P4_KT * 32) + kso);
-    v = *(const u32x4*)(Vg + t * P4_KT + vso);
+    if constexpr (F8 != 0) v = *(const u32x2*)(Vg8 + t * P4_KT + vso);
+    else v = *(const u32x4*)(Vg + t * P4_KT + vso);
   };
-  auto lstore = [&](unsigned char* slot, const u32x4& k, const u32x4& v) __attribute__((always_inline)) {
+  auto lstore = [&](unsigned char* slot, const u32x4& k, const VStage& v) __attribute__((always_inline)) {
     *(u32x4*)(slot + kw) = k;
-    *(u32x4*)(slot + vw) = v;
+    *(VStage*)(slot + vw) = v;
   };
-  auto mask_pad = [&](u32x4& k, u32x4& v) {  // this thread's staging share of tile nfull, keys >= nk -> 0
+  auto mask_pad = [&](u32x4& k, VStage& v) {  // this thread's staging share of tile nfull, keys >= nk -> 0
     const int k0 = nfull * P4_KT;
     if (k0 + krow >= p.nk) k = u32x4{0u, 0u, 0u, 0u};
-    bf16x8 e = __builtin_bit_cast(bf16x8, v);
+    if constexpr (F8 != 0) {
+      uint64_t e = __builtin_bit_cast(uint64_t, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (k0 + vc * 8 + j >= p.nk) e[j] = (bf16)0.0f;
-    v = __builtin_bit_cast(u32x4, e);
+      for (int j = 0; j < 8; ++j)
+        if (k0 + vc * 8 + j >= p.nk) e &= ~((uint64_t)0xff << (8 * j));
+      v = __builtin_bit_cast(u32x2, e);
+    } else {
+      bf16x8 e = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (k0 + vc * 8 + j >= p.nk) e[j] = (bf16)0.0f;
+      v = __builtin_bit_cast(u32x4, e);
+    }
   };
   // one barrier per tile: the LDS writes done (lgkmcnt(0)), global loads left in flight
   auto lds_barrier = [&]() __attribute__((always_inline)) {
@@ -233,12 +287,14 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
 
   // row-sum selector (A of v_mfma_f32_16x16x32_bf16): D row 0 sums the P fragment's k-groups 0 and 2
   // (queries 0-15 of the chain), row 1 k-groups 1 and 3 (queries 16-31)
+  // (F8: A of v_mfma_scale_f32_16x16x128_f8f6f4 in e4m3, the same rows over k-groups of 32)
   bf16x8 sel;
+  i32x8 sel8;
   {
     const int m = lane & 15, kg = lane >> 4;
     const bool one = (m == 0 && (kg & 1) == 0) || (m == 1 && (kg & 1) == 1);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sel[j] = (bf16)(one ? 1.0f : 0.0f);
+    for (int j = 0; j < 8; ++j) sel[j] = (bf16)(one ? 1.0f : 0.0f), sel8[j] = one ? 0x38383838 : 0;  // e4m3 1.0
   }
 
   f32x16 o[P4_NCH];
@@ -266,7 +322,8 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       s[u] = mfma32(kf[u][1], qf[qb][1], s[u]);
     }
   };
-  auto expc = [&](bf16x8(&pb)[2][2], const f32x16(&s)[2]) __attribute__((always_inline)) {
+  // bf16 P.V of one (tile, chain): the re-run tile of every variant
+  auto expc16 = [&](bf16x8(&pb)[2][2], const f32x16(&s)[2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -274,7 +331,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) pb[u][sp][j] = (bf16)__builtin_amdgcn_exp2f(s[u][8 * sp + j]);
   };
-  auto pv = [&](int qb, const bf16x8(&pb)[2][2], const bf16x8(&vf)[2][2]) __attribute__((always_inline)) {
+  auto pv16 = [&](int qb, const bf16x8(&pb)[2][2], const bf16x8(&vf)[2][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -282,6 +339,49 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
         o[qb] = mfma32(vf[u][sp], pb[u][sp], o[qb]);
         lacc[qb] = mfma16(sel, pb[u][sp], lacc[qb]);
       }
+  };
+  // F8: per-chain conversion scale of the lane's query (P' = exp2(s) / scale), set from the first tile
+  // and P'(0), the value every padded key adds to the row sum
+  float scl[P4_NCH] = {1.0f, 1.0f}, padv[P4_NCH] = {1.0f, 1.0f};
+  // bf16: P^T fragment (u, sp) = keys 32u + 16sp + 8hh + 0..7 (bf16x8 each).  F8: one i32x8 per chain,
+  // byte 16u + i of the lane = s[u][i], i.e. logical k 32hh + 16u + i = key 32u + 16 (i >> 3) + 8hh + (i & 7)
+  auto expc = [&](PFrag& pb, const f32x16(&s)[2], int qb) __attribute__((always_inline)) {
+    if constexpr (F8 != 0) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          // (the low half is converted into the register of its own first input, which dies there: both
+          // halves get written, and any other `old` operand costs a v_mov per word)
+          const float e0 = __builtin_amdgcn_exp2f(s[u][4 * w]);
+          s16x2 x = P8<F8>::cvt(__builtin_bit_cast(s16x2, e0), e0, __builtin_amdgcn_exp2f(s[u][4 * w + 1]), scl[qb],
+                                false);
+          x = P8<F8>::cvt(x, __builtin_amdgcn_exp2f(s[u][4 * w + 2]), __builtin_amdgcn_exp2f(s[u][4 * w + 3]), scl[qb],
+                          true);
+          pb[4 * u + w] = __builtin_bit_cast(int, x);
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[u][sp][j] = (bf16)__builtin_amdgcn_exp2f(s[u][8 * sp + j]);
+    }
+  };
+  auto pv = [&](int qb, const PFrag& pb, const VFrag& vf) __attribute__((always_inline)) {
+    if constexpr (F8 != 0) {
+      o[qb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pb, o[qb], 0, P8<F8>::FMT, 0, 127, 0, 127);
+      lacc[qb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(sel8, pb, lacc[qb], 0, P8<F8>::FMT, 0, 127, 0, 127);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          o[qb] = mfma32(vf[u][sp], pb[u][sp], o[qb]);
+          lacc[qb] = mfma16(sel, pb[u][sp], lacc[qb]);
+        }
+    }
   };
   // the order of one pipeline step: 12 MFMAs (S0-S3 32x32, then P.V 32x32 / row-sum 16x16 pairs), 32
   // exps, 16 conversions and the step's LDS / global traffic.  An MFMA holds vector issue for 8 cycles;
@@ -309,6 +409,26 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       __builtin_amdgcn_sched_group_barrier(SG_VALU, 2, 0);
     }
 #else
+    if constexpr (F8 != 0) {
+      // S MFMAs (32 cycles): 3 exps each; P.V 32x32x64 (64 cycles): 7; row sum 16x16x128 (32 cycles): 3
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+        if (mem && i < 2) __builtin_amdgcn_sched_group_barrier(SG_DS_READ, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_TRANS, 3, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_TRANS, 7, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_TRANS, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_TRANS, 10, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_VALU, 16, 0);
+      if (mem) {
+        __builtin_amdgcn_sched_group_barrier(SG_DS_WRITE, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_VMEM_READ, 2, 0);
+      }
+      return;
+    }
     // S MFMAs: 3 exps each (the LDS reads of the next fragments ride in the first two gaps)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -340,11 +460,13 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   //   step (t, 1): S(t+1, chain 0) | exp S(t, chain 1) | P.V(t, chain 0); then the tile's barrier
   // kf(t) in register set t % 2, vf(t) in set (t + 1) % 2
   if (ntiles > 0) {
-    bf16x8 kf[2][2][2], vf[2][2][2];
+    bf16x8 kf[2][2][2];
+    VFrag vf[2];
     f32x16 sa[2], sb[2];
-    bf16x8 pa[2][2], pz[2][2];
+    PFrag pa, pz;
     {  // tiles 0 and 1 in flight together, then tile 2 into the staging registers
-      u32x4 rk1, rv1;
+      u32x4 rk1;
+      VStage rv1;
       gload(tile_of(0), rk, rv);
       gload(tile_of(min(1, ntiles - 1)), rk1, rv1);
       if (partial) mask_pad(rk, rv);
@@ -365,13 +487,49 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       return;  // no barrier follows the fast pass
     }
     readk(kf[0], ring);
+    if constexpr (F8 != 0) {
+      vf[0] = i32x8{0, 0, 0, 0, 0, 0, 0, 0}, pz = vf[0];
+    } else {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int sp = 0; sp < 2; ++sp)
+        for (int sp = 0; sp < 2; ++sp)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) vf[0][u][sp][j] = pz[u][sp][j] = (bf16)0.0f;
+          for (int j = 0; j < 8; ++j) vf[0][u][sp][j] = pz[u][sp][j] = (bf16)0.0f;
+    }
     smm(sa, kf[0], 0);
+    if constexpr (F8 != 0) {
+      // the lane's query reference: max over the real keys of the first tile in processing order (both
+      // chains; chain 1's scores are recomputed by the loop), P' = exp2(s) / 2^e, e = floor(max) - ETOP.  The
+      // row sums start at -npad P'(0): the padded keys (s = 0) add exactly that, as fp8 (0 once 2^-e
+      // underflows); with padded keys e >= -EMAX keeps P'(0) inside the format (a row whose first-tile max is
+      // that far below 0 keeps fewer octaves under its max; a total underflow fails the row-sum check)
+      f32x16 s1[2];
+      smm(s1, kf[0], 1);
+      const int k0 = tile_of(0) * P4_KT;
+#pragma unroll
+      for (int qb = 0; qb < P4_NCH; ++qb) {
+        const f32x16(&s)[2] = qb == 0 ? sa : s1;
+        float m = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (k0 + 32 * u + 16 * (i >> 3) + 8 * hh + (i & 7) < p.nk) m = fmaxf(m, s[u][i]);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+        m = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        const float elo = partial ? -(float)P8<F8>::EMAX : -100.f;
+        const int e = (int)fminf(fmaxf(floorf(m) - (float)P8<F8>::ETOP, elo), 100.f);
+        scl[qb] = __int_as_float((e + 127) << 23);
+        padv[qb] = -e >= P8<F8>::EMIN ? __int_as_float((127 - e) << 23) : 0.f;
+      }
+      const float ps = -(float)(ntiles * P4_KT - p.nk);
+#pragma unroll
+      for (int qb = 0; qb < P4_NCH; ++qb) {
+        const float own = ps * padv[qb], hi = __shfl(own, (lane & 15) + 16, 64);
+        lacc[qb] = f32x4{own, hi, own, hi};
+      }
+    }
     // tile t in ring slot t % 4 (compile-time slots: every LDS address is a base + an immediate)
     auto iter = [&](auto phc, int t) __attribute__((always_inline)) {
       constexpr int L = decltype(phc)::value, A = L & 1, B = A ^ 1;
@@ -381,11 +539,11 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       lstore(ring + S2, rk, rv);
       gload(tile_of(min(t + 3, ntiles - 1)), rk, rv);
       smm(sb, kf[A], 1);
-      expc(pa, sa);
+      expc(pa, sa, 0);
       pv(1, pz, vf[A]);
       pin_step(true);
       smm(sa, kf[B], 0);
-      expc(pz, sb);
+      expc(pz, sb, 1);
       pv(0, pa, vf[B]);
       pin_step(false);
       lds_barrier();
@@ -451,8 +609,8 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
         for (int i = 0; i < 16; ++i) s[0][i] -= mref[qb], s[1][i] -= mref[qb];
       }
       bf16x8 pb[2][2];
-      expc(pb, s);
-      pv(qb, pb, vf);
+      expc16(pb, s);
+      pv16(qb, pb, vf);
     }
   };
 
@@ -471,7 +629,8 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     for (int qb = 0; qb < P4_NCH; ++qb) {
       const float rs = rowsum(qb);
       const unsigned lb = __float_as_uint(rs) & 0x7fffffffu;
-      bad |= lb >= 0x71800000u || lb < 0x21800000u || rs < padsum * 0x1p-12f;
+      // (F8: the padded keys' ones are P'(0) each; a score past the format's range is NaN / inf here)
+      bad |= lb >= 0x71800000u || lb < 0x21800000u || rs < padsum * padv[qb] * 0x1p-12f;
     }
     if (__any(bad)) {
       zero_acc();
@@ -513,7 +672,42 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
 }  // namespace
 
 hipError_t launch_attn_pipe(const Attn2Args& a, hipStream_t st) {
-  hipLaunchKernelGGL(attn_pipe_kernel, dim3(a.nblocks), dim3(256), 0, st, a);
+  if (a.f8 == 1) {
+    if (!a.vt8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(attn_pipe_kernel<1>, dim3(a.nblocks), dim3(256), 0, st, a);
+  } else if (a.f8 == 2) {
+    if (!a.vt8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(attn_pipe_kernel<2>, dim3(a.nblocks), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(attn_pipe_kernel<0>, dim3(a.nblocks), dim3(256), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
+namespace {
+// bf16 -> e4m3 (saturating at +-448: a value past the range must not turn V into NaN), 8 elements per
+// thread, for the F8 attention's V^T operand
+__global__ void vt_fp8_kernel(const u32x4* __restrict__ in, u32x2* __restrict__ out, int64_t n8) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  const bf16x8 v = __builtin_bit_cast(bf16x8, in[i]);
+  float f[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf((float)v[j], -448.f), 448.f);
+  s16x2 lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(s16x2{0, 0}, f[0], f[1], 1.0f, false);
+  lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(lo, f[2], f[3], 1.0f, true);
+  s16x2 hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(s16x2{0, 0}, f[4], f[5], 1.0f, false);
+  hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(hi, f[6], f[7], 1.0f, true);
+  out[i] = u32x2{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
+}
+}  // namespace
+
+hipError_t launch_vt_fp8(const void* vt, void* vt8, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (n % 8) return hipErrorInvalidValue;
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(vt_fp8_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st, (const u32x4*)vt, (u32x2*)vt8,
+                     n8);
   return hipGetLastError();
 }
 

@@ -77,15 +77,17 @@ struct mmpfn_ctx {
   // workspace of the selected lane (per-member forward state)
   DevBuf ws_X, ws_O, ws_big, ws_pe, ws_slots, ws_scr, ws_flag;
   DevBuf mx[8];
-  // current forward geometry (M members of equal geometry stacked as [M][T][S][E])
-  int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0, M = 1;
+  DevBuf tap_v8;  // e4m3 V^T of the fp8 attention tap
+  // current forward geometry (M members of equal geometry stacked as [M][T][S][E]); f8: the fp8 P.V
+  // variant of the item attention (f8_of of the forward's precision code; prec holds its base_prec)
+  int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0, M = 1, f8 = 0;
   bool embedded = false;
   // lanes: independent forward workspaces sharing the weights, so members can run
   // concurrently on different streams; the selected lane lives in the fields above and the
   // others are parked here (mmpfn_select_lane swaps them)
   struct Lane {
     DevBuf ws_X, ws_O, ws_big, ws_pe, ws_slots, ws_scr, ws_flag;
-    int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0, M = 1;
+    int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0, M = 1, f8 = 0;
     bool embedded = false;
   };
   std::vector<Lane> lanes;  // lanes[cur] is stale while cur is selected
@@ -105,6 +107,7 @@ struct mmpfn_ctx {
     std::swap(a.ws_flag, b.ws_flag);
     std::swap(a.S, b.S), std::swap(a.T, b.T), std::swap(a.N, b.N), std::swap(a.G, b.G), std::swap(a.C, b.C);
     std::swap(a.Npad, b.Npad), std::swap(a.prec, b.prec), std::swap(a.embedded, b.embedded), std::swap(a.M, b.M);
+    std::swap(a.f8, b.f8);
   }
 };
 
@@ -456,7 +459,9 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
   if (S <= 0 || N <= 0 || N > S || (x && F <= 0) || C < 0 || U <= 0)
     return fail(ctx, MMPFN_ERR_INVALID, "bad forward geometry");
   if (!x && C == 0) return fail(ctx, MMPFN_ERR_INVALID, "no input tokens");
-  if (prec != PREC_F32 && prec != PREC_BF16 && prec != PREC_F32_MFMA) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  if (!prec_ok(prec)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  const int f8 = f8_of(prec);
+  prec = base_prec(prec);
   const int E = d.emsize, fpg = d.features_per_group;
   const int G = x ? (F + fpg - 1) / fpg : 0;
   const int T = G + C + 1;
@@ -466,6 +471,7 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
   int* flag;
   if (m == 0) {
     ctx->S = S, ctx->T = T, ctx->N = N, ctx->G = G, ctx->C = C, ctx->Npad = Npad, ctx->prec = prec, ctx->M = M;
+    ctx->f8 = f8;
     RC(ensure(ctx, ctx->ws_X, (size_t)M * R * E * 4));
     RC(ensure(ctx, ctx->ws_O, (size_t)M * R * E * 4));
     const size_t Tpad = (T + 63) / 64 * 64;
@@ -479,7 +485,8 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
     HIPCHK(launch_pos_emb(pos_rand, G + C, (const float*)ctx->pe_w.p, (const float*)ctx->pe_b.p,
                           (float*)ctx->ws_pe.p, E, st));
   } else {
-    if (S != ctx->S || T != ctx->T || N != ctx->N || G != ctx->G || C != ctx->C || prec != ctx->prec || m >= ctx->M)
+    if (S != ctx->S || T != ctx->T || N != ctx->N || G != ctx->G || C != ctx->C || prec != ctx->prec || f8 != ctx->f8 ||
+        m >= ctx->M)
       return fail(ctx, MMPFN_ERR_INVALID, "batched members must share S, N, F, C and precision");
     flag = (int*)ctx->ws_flag.p;
   }
@@ -511,6 +518,7 @@ int embed_cached(mmpfn_ctx* ctx, const mmpfn_cache* cc, const float* x, int S, i
   const size_t R = (size_t)S * T;
   hipStream_t st = ctx->stream;
   ctx->S = S, ctx->T = T, ctx->N = 0, ctx->G = G, ctx->C = C, ctx->Npad = 0, ctx->prec = prec, ctx->M = 1;
+  ctx->f8 = 0;  // the cache keeps bf16 V^T: its test rows run the bf16 P.V
   RC(ensure(ctx, ctx->ws_X, R * E * 4));
   RC(ensure(ctx, ctx->ws_O, R * E * 4));
   const size_t Tpad = (T + 63) / 64 * 64;
@@ -597,7 +605,7 @@ int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int S, int T, in
 //      fuse_out: the out-projection + residual + LN is left to the MLP kernel's prologue (the
 //      attention output stays in ws_O); otherwise X <- LN(X + O Wout^T) here.
 int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int Npad, int M, int prec,
-                  bool fuse_out) {
+                  bool fuse_out, int f8 = 0) {
   const mmpfn_model_desc& d = ctx->d;
   const LayerW& L = ctx->layers[l];
   const int E = d.emsize, H = d.nhead, Q = S - N;
@@ -678,9 +686,14 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
         ev = &ctx->kt_pool[ctx->kt_used];
         ctx->kt_used += 2;
         ctx->kt_flops += 4.0 * TM * (double)(N + Q) * N * E;
-        HIPCHK(hipEventRecord(ev[0], st));
       }
-      HIPCHK(launch_attn_layer(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st, 0, true));
+      void* V8 = nullptr;
+      if (f8) {  // e4m3 V^T after the bf16 one (ws_big holds twice the bf16 Q / K / V^T bytes)
+        V8 = (unsigned char*)Vi + (size_t)TM * H * Npad * 32 * eb;
+        HIPCHK(launch_vt_fp8(Vi, V8, (int64_t)TM * H * Npad * 32, st));
+      }
+      if (ev) HIPCHK(hipEventRecord(ev[0], st));
+      HIPCHK(launch_attn_layer(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st, 0, true, V8, f8));
       if (ev) HIPCHK(hipEventRecord(ev[1], st));
     } else if (prec == PREC_F32) {  // parity mode: split-bf16 products, train and test rows in one launch
       HIPCHK(launch_attn_item3(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st));
@@ -728,7 +741,7 @@ int run_layer(mmpfn_ctx* ctx, int l) {
   float* Xall = (float*)ctx->ws_X.p;
   const bool fuse = mlp_fuses_out(ctx->d, prec);
   RC(feat_sublayer(ctx, L, Xall, S, T, M, prec));
-  RC(item_sublayer(ctx, l, Xall, S, T, N, Npad, M, prec, fuse));
+  RC(item_sublayer(ctx, l, Xall, S, T, N, Npad, M, prec, fuse, ctx->f8));
   return mlp_sublayer(ctx, L, Xall, (int64_t)S * T * M, prec, fuse ? ctx->ws_O.p : nullptr);
 }
 
@@ -918,7 +931,7 @@ void mmpfn_destroy(mmpfn_ctx* ctx) {
                     &ctx->cap_f3, &ctx->cap_f3_h, &ctx->cap_f3_b, &ctx->cap_ng, &ctx->cap_nb, &ctx->moe_w1,
                     &ctx->moe_w1_h, &ctx->moe_b1, &ctx->moe_w2, &ctx->moe_w2_h, &ctx->moe_b2, &ctx->moe_gw,
                     &ctx->moe_gb, &ctx->ws_X, &ctx->ws_O, &ctx->ws_big, &ctx->ws_pe, &ctx->ws_slots, &ctx->ws_scr,
-                    &ctx->ws_flag})
+                    &ctx->ws_flag, &ctx->tap_v8})
     fr(*b);
   for (auto& b : ctx->mx) fr(b);
   for (auto& kv : ctx->split) fr(kv.second);
@@ -998,8 +1011,9 @@ int mmpfn_mixer_tokens(const mmpfn_ctx* ctx, int n_mod) {
 int mmpfn_mixer_forward(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int precision) {
   if (!ctx || !image || !tokens || S <= 0 || n_mod <= 0) return MMPFN_ERR_INVALID;
   if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
+  if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
-  return mixer(ctx, image, S, n_mod, tokens, precision);
+  return mixer(ctx, image, S, n_mod, tokens, base_prec(precision));
 }
 
 int mmpfn_embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int C, const float* y, int N,
@@ -1097,7 +1111,8 @@ int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const voi
   if (s0 < 0 || nq < 0 || s0 + nq > S || nk <= 0 || nk > Npad || Npad % 64 || H <= 0 || T <= 0 || kvh >= H)
     return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
   HIPCHK(hipSetDevice(ctx->device));
-  HIPCHK(launch_attn_item(q, k, vt, out, S, T, H, Npad, s0, nq, nk, kvh, precision, ctx->stream));
+  if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  HIPCHK(launch_attn_item(q, k, vt, out, S, T, H, Npad, s0, nq, nk, kvh, base_prec(precision), ctx->stream));
   return MMPFN_OK;
 }
 
@@ -1106,6 +1121,8 @@ int mmpfn_cache_build(mmpfn_ctx* ctx, const float* x, int N, int F, const float*
   if (!ctx || !out || !y_train || !uniq || !pos_rand) return MMPFN_ERR_INVALID;
   *out = nullptr;
   HIPCHK(hipSetDevice(ctx->device));
+  if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  precision = base_prec(precision);  // the cache keeps bf16 K / V^T: fp8 P.V codes build a bf16 cache
   RC(embed(ctx, x, N, F, tokens, C, y_train, N, uniq, U, pos_rand, precision));
   const mmpfn_model_desc& d = ctx->d;
   const int E = d.emsize, fpg = d.features_per_group, eb = precision == PREC_BF16 ? 2 : 4;
@@ -1208,6 +1225,20 @@ int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, con
   return MMPFN_OK;
 }
 
+int mmpfn_item_attention_layer_fp8(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
+                                   int T, int H, int Npad, int N, int p_format) {
+  if (!ctx || !q || !k || !vt || !out) return MMPFN_ERR_INVALID;
+  if (N <= 0 || N > S || N > Npad || Npad % 64 || H <= 0 || H > 8 || T <= 0 || (p_format != 1 && p_format != 2))
+    return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
+  HIPCHK(hipSetDevice(ctx->device));
+  const int64_t n = (int64_t)T * H * 32 * Npad;
+  RC(ensure(ctx, ctx->tap_v8, (size_t)n));
+  HIPCHK(launch_vt_fp8(vt, ctx->tap_v8.p, n, ctx->stream));
+  HIPCHK(launch_attn_layer(q, k, vt, out, S, T, H, Npad, N, 0, N, N, S - N, 0, ctx->stream, 0, false, ctx->tap_v8.p,
+                           p_format));
+  return MMPFN_OK;
+}
+
 int mmpfn_item_attention_cached(mmpfn_ctx* ctx, const void* q, const void* k0, const void* vt0, void* out, int S,
                                 int T, int H, int Npad, int N) {
   if (!ctx || !q || !k0 || !vt0 || !out) return MMPFN_ERR_INVALID;
@@ -1223,8 +1254,7 @@ static int tap_check(mmpfn_ctx* ctx, int layer, const void* X, int precision) {
   if (!ctx || !X) return MMPFN_ERR_INVALID;
   if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
   if (layer < 0 || layer >= ctx->d.nlayers) return fail(ctx, MMPFN_ERR_INVALID, "bad layer index");
-  if (precision != PREC_F32 && precision != PREC_BF16 && precision != PREC_F32_MFMA)
-    return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
   return MMPFN_OK;
 }
@@ -1233,7 +1263,7 @@ int mmpfn_feature_attention(mmpfn_ctx* ctx, int layer, float* X, int S, int T, i
   RC(tap_check(ctx, layer, X, precision));
   if (S <= 0 || T <= 0) return fail(ctx, MMPFN_ERR_INVALID, "bad state geometry");
   RC(tap_workspace(ctx, S, T, 64));
-  return feat_sublayer(ctx, ctx->layers[layer], X, S, T, 1, precision);
+  return feat_sublayer(ctx, ctx->layers[layer], X, S, T, 1, base_prec(precision));
 }
 
 int mmpfn_item_attention_block(mmpfn_ctx* ctx, int layer, float* X, int S, int T, int N, int precision) {
@@ -1241,13 +1271,13 @@ int mmpfn_item_attention_block(mmpfn_ctx* ctx, int layer, float* X, int S, int T
   if (S <= 0 || T <= 0 || N <= 0 || N > S) return fail(ctx, MMPFN_ERR_INVALID, "bad state geometry");
   const int Npad = (N + 63) / 64 * 64;
   RC(tap_workspace(ctx, S, T, Npad));
-  return item_sublayer(ctx, layer, X, S, T, N, Npad, 1, precision, false);
+  return item_sublayer(ctx, layer, X, S, T, N, Npad, 1, base_prec(precision), false, f8_of(precision));
 }
 
 int mmpfn_mlp_ln(mmpfn_ctx* ctx, int layer, float* X, int64_t rows, int precision) {
   RC(tap_check(ctx, layer, X, precision));
   if (rows <= 0) return fail(ctx, MMPFN_ERR_INVALID, "bad row count");
-  return mlp_sublayer(ctx, ctx->layers[layer], X, rows, precision, nullptr);
+  return mlp_sublayer(ctx, ctx->layers[layer], X, rows, base_prec(precision), nullptr);
 }
 
 int mmpfn_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int precision) {
@@ -1255,20 +1285,18 @@ int mmpfn_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* token
   if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
   if (ctx->d.mixer_type != MMPFN_MIXER_MGM && ctx->d.mixer_type != MMPFN_MIXER_MGM_CAP)
     return fail(ctx, MMPFN_ERR_INVALID, "model has no MGM head bank");
-  if (precision != PREC_F32 && precision != PREC_BF16 && precision != PREC_F32_MFMA)
-    return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
-  return mixer_mgm(ctx, image, S, n_mod, tokens, precision);
+  return mixer_mgm(ctx, image, S, n_mod, tokens, base_prec(precision));
 }
 
 int mmpfn_cap(mmpfn_ctx* ctx, const float* mgm_tokens, int S, int M, float* tokens, int precision) {
   if (!ctx || !mgm_tokens || !tokens || S <= 0 || M <= 0) return MMPFN_ERR_INVALID;
   if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
   if (ctx->d.mixer_type != MMPFN_MIXER_MGM_CAP) return fail(ctx, MMPFN_ERR_INVALID, "model has no CAP");
-  if (precision != PREC_F32 && precision != PREC_BF16 && precision != PREC_F32_MFMA)
-    return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
-  return mixer_cap(ctx, mgm_tokens, S, M, tokens, precision);
+  return mixer_cap(ctx, mgm_tokens, S, M, tokens, base_prec(precision));
 }
 
 }  // extern "C"

@@ -11,7 +11,13 @@ namespace mmpfn {
 // bf16 hi + lo planes, x = hi + lo to 2^-17, and the three significant products hi.hi + hi.lo +
 // lo.hi accumulated in fp32 (the dropped lo.lo term is 2^-16 relative) -- 3 bf16 MFMAs at 16x the
 // fp32-input rate; PREC_F32_MFMA: the same forward on fp32-input MFMA (exact fp32 fma chains)
-enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1, PREC_F32_MFMA = 2 };
+// PREC_BF16_F8 / PREC_BF16_F8E5: PREC_BF16 with the sample-axis attention's P.V on block-scaled fp8
+// MFMA (V^T e4m3; P e4m3 / e5m2; attention_pipe.hip) -- config E's fp8 path, opt-in
+enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1, PREC_F32_MFMA = 2, PREC_BF16_F8 = 3, PREC_BF16_F8E5 = 4 };
+// the precision the layer kernels run in, and the fp8 P.V variant (0: none)
+inline int base_prec(int p) { return p == PREC_BF16_F8 || p == PREC_BF16_F8E5 ? PREC_BF16 : p; }
+inline int f8_of(int p) { return p == PREC_BF16_F8 ? 1 : p == PREC_BF16_F8E5 ? 2 : 0; }
+inline bool prec_ok(int p) { return p >= PREC_F32 && p <= PREC_BF16_F8E5; }
 
 enum Epi : int {
   EPI_STORE = 0,      // C[row] = act(acc + bias)
@@ -150,6 +156,8 @@ struct Attn2Args {
   int64_t kv_bstride;  // elements between the K (V^T) blocks of consecutive columns: H*Npad*32, or
                        // Npad*32 for a head-0-only train-KV cache
   int q_prescaled;     // Q already carries log2(e)/sqrt(32) (folded into the engine's bf16 Q weights)
+  const unsigned char* vt8;  // f8 != 0: V^T in e4m3, the layout of vt
+  int f8;              // P.V on fp8 MFMA: 0 off (bf16), 1 P in e4m3, 2 P in e5m2 (attention_pipe.hip)
 };
 // software-pipelined bf16 sample-axis attention (attention_pipe.hip); tasks of ATTN_ITEM_QPB queries
 constexpr int ATTN_ITEM_QPB = 256;
@@ -159,9 +167,14 @@ hipError_t launch_attn_pipe(const Attn2Args& a, hipStream_t st);
 //   every head against K/V head kvb (nb = 0: none); keys [0, nk), Npad % 64 == 0.
 //   kv_bstride > 0: K / V^T hold head 0 only, column blocks kv_bstride elements apart (train-KV
 //   cache; then na = 0 and kvb = 0)
+//   f8 != 0: P.V and the row sums on block-scaled fp8 MFMA with vt8 = V^T in e4m3 (launch_vt_fp8), P in
+//   e4m3 (1) or e5m2 (2); vt (bf16) still serves the exact re-run path
 hipError_t launch_attn_layer(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0,
-                             bool q_prescaled = false);  // Q already scaled by log2(e)/sqrt(32)
+                             bool q_prescaled = false,  // Q already scaled by log2(e)/sqrt(32)
+                             const void* vt8 = nullptr, int f8 = 0);
+// bf16 -> e4m3 (saturating) of n elements (n % 8 == 0): the F8 attention's V^T operand
+hipError_t launch_vt_fp8(const void* vt, void* vt8, int64_t n, hipStream_t st);
 // parity mode (PREC_F32) of launch_attn_layer on fp32 Q / K / V^T (split bf16 three-product MFMAs), fp32 O
 hipError_t launch_attn_item3(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0);

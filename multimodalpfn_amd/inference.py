@@ -36,7 +36,7 @@ from multimodalpfn_amd.utils import infer_random_state
 
 def _precision(model, device: torch.device, autocast: bool, forced: torch.dtype | None) -> int:
     if forced is not None:
-        return _lib.f32_precision() if forced in (torch.float32, torch.float64) else _lib.PREC_BF16
+        return _lib.precision_of_dtype(forced)
     return _lib.PREC_BF16 if (autocast and device.type == "cuda") else _lib.f32_precision()
 
 

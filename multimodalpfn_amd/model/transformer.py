@@ -340,7 +340,7 @@ class PerFeatureTransformer(nn.Module):
 
     def precision(self, device: torch.device) -> int:
         if self._forced_dtype is not None:
-            return _lib.f32_precision() if self._forced_dtype in (torch.float32, torch.float64) else _lib.PREC_BF16
+            return _lib.precision_of_dtype(self._forced_dtype)
         if torch.is_autocast_enabled(device.type):
             return _lib.PREC_BF16
         return _lib.f32_precision()

@@ -64,7 +64,7 @@ def _blocks(body: str) -> list[collections.Counter]:
 def test_attention_tile_bodies_have_no_register_shuffles():
     """The pipelined loop (attention_pipe.hip) is one basic block of six tiles: per tile 64 v_exp_f32,
     32 v_cvt_pk_bf16_f32, 16 + 8 MFMAs and a handful of address / loop ops, no register shuffles."""
-    body = _function(_asm("attention_pipe.hip", ["-fno-honor-nans"]), "attn_pipe_kernel")
+    body = _function(_asm("attention_pipe.hip", ["-fno-honor-nans"]), "attn_pipe_kernelILi0E")
     loops = [c for c in _blocks(body) if c["v_exp_f32_e32"] >= 256 and c["v_exp_f32_e32"] % 64 == 0
              and c["v_mfma_f32_32x32x16_bf16"] * 4 == c["v_exp_f32_e32"] and c["v_cndmask_b32_e64"] == 0]
     assert len(loops) == 1, [(c["v_exp_f32_e32"], c["v_mfma_f32_32x32x16_bf16"]) for c in _blocks(body)]
@@ -73,6 +73,24 @@ def test_attention_tile_bodies_have_no_register_shuffles():
     valu = sum(v for k, v in c.items() if k.startswith("v_") and not k.startswith("v_mfma"))
     movs = c["v_mov_b32_e32"] + c["v_mov_b64_e32"]
     assert c["v_mfma_f32_16x16x32_bf16"] == 8 * tiles and c["v_cvt_pk_bf16_f32"] == 32 * tiles
+    assert movs <= tiles and valu <= 100 * tiles, (valu, movs)
+
+
+@pytest.mark.parametrize("variant,cvt", [(1, "v_cvt_scalef32_pk_fp8_f32"), (2, "v_cvt_scalef32_pk_bf8_f32")])
+def test_fp8_attention_tile_bodies(variant, cvt):
+    """The fp8 P.V variants (config E): per tile 64 exps, 8 score MFMAs (bf16), one 32x32x64 P.V and one
+    16x16x128 row-sum MFMA per chain (block-scaled f8f6f4), 32 scaled conversions, no register shuffles
+    (a defined `old` word of the packed conversions once cost 16 v_mov per tile)."""
+    body = _function(_asm("attention_pipe.hip", ["-fno-honor-nans"]), f"attn_pipe_kernelILi{variant}E")
+    loops = [c for c in _blocks(body) if c["v_exp_f32_e32"] >= 256 and c["v_exp_f32_e32"] % 64 == 0
+             and c["v_mfma_f32_32x32x16_bf16"] * 8 == c["v_exp_f32_e32"]]
+    assert len(loops) == 1, [(c["v_exp_f32_e32"], c["v_mfma_f32_32x32x16_bf16"]) for c in _blocks(body)]
+    c = loops[0]
+    tiles = c["v_exp_f32_e32"] // 64
+    valu = sum(v for k, v in c.items() if k.startswith("v_") and not k.startswith("v_mfma"))
+    movs = c["v_mov_b32_e32"] + c["v_mov_b64_e32"]
+    assert c["v_mfma_scale_f32_32x32x64_f8f6f4"] == 2 * tiles and c["v_mfma_scale_f32_16x16x128_f8f6f4"] == 2 * tiles
+    assert c[cvt] == 32 * tiles and c["v_cvt_pk_bf16_f32"] == 0
     assert movs <= tiles and valu <= 100 * tiles, (valu, movs)
 
 

@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 F32_TOL = 1e-4
 LARGE_BF16_TOL = {"B": 2.5e-2, "E": 3.5e-2}  # measured 1.28e-2 and 1.80e-2 (profiles/r02)
 BF16_AGREE = 0.995  # argmax agreement; measured 1.00 on every golden and on B / E (profiles/r02)
+F8_TOL = 5e-2  # config E with the fp8 P.V (MMPFN_PREC_BF16_F8 / _F8E5) against the oracle
 BF16_TOL = 2e-2  # measured 3.1e-3 .. 9.5e-3 over the goldens (profiles/r02/pytest_gpu_r02a.log)
 
 
@@ -139,7 +140,8 @@ def _attn_ref(q, k, v):
     return torch.softmax(s, -1) @ v.double()
 
 
-ATTN_TOL = {0: 5e-5, 1: 2e-2, 2: 2e-5}  # parity (split bf16), bf16, fp32-input MFMA; |O| <= ~1
+# parity (split bf16), bf16, fp32-input MFMA, fp8 P.V with P e4m3 / e5m2 (V^T e4m3); |O| <= ~1
+ATTN_TOL = {0: 5e-5, 1: 2e-2, 2: 2e-5, 3: 1e-1, 4: 1e-1}
 
 
 @pytest.mark.parametrize("prec", [0, 1, 2])
@@ -207,12 +209,15 @@ def _launch_layer(q, k, v, Npad, N, prec=1):
     vt[:, :, :, :N] = v.transpose(-1, -2)
     lib = _lib.load_library()
     ctx = lib.mmpfn_create(0, None)
-    dt = torch.bfloat16 if prec == 1 else torch.float32
+    dt = torch.bfloat16 if prec in (1, 3, 4) else torch.float32
     qd, kd, vd = q.to("cuda", dt), kp.to("cuda", dt), vt.to("cuda", dt)
     out = torch.zeros(T, S, H * d, device="cuda", dtype=dt)
     if prec == 1:
         assert lib.mmpfn_item_attention_layer(ctx, qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), S, T,
                                               H, Npad, N) == 0
+    elif prec in (3, 4):  # fp8 P.V: P in e4m3 (3) / e5m2 (4), V^T e4m3
+        assert lib.mmpfn_item_attention_layer_fp8(ctx, qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), S,
+                                                  T, H, Npad, N, prec - 2) == 0
     else:
         assert lib.mmpfn_item_attention(ctx, qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), S, T, H,
                                         Npad, 0, N, N, -1, prec) == 0
@@ -226,7 +231,7 @@ def _launch_layer(q, k, v, Npad, N, prec=1):
 
 def _layer_ref(q, k, v, N, prec=1):
     T, H, S, d = q.shape
-    dt = torch.bfloat16 if prec == 1 else torch.float32
+    dt = torch.bfloat16 if prec in (1, 3, 4) else torch.float32
     qr, kr, vr = (t.to(dt).float() for t in (q, k, v))
     ref_tr = _attn_ref(qr[:, :, :N], kr, vr)
     ref_te = _attn_ref(qr[:, :, N:], kr[:, :1].expand_as(kr), vr[:, :1].expand_as(vr))
@@ -243,7 +248,23 @@ def test_item_attention_layer_fused(S, N, T):
     assert (got.double() - ref).abs().max().item() < 2e-2
 
 
-@pytest.mark.parametrize("prec", [1, 0])
+@pytest.mark.parametrize("prec", [3, 4])
+@pytest.mark.parametrize("S,N,T", [(2298, 1838, 2), (70, 1, 2), (130, 64, 1), (200, 65, 3), (700, 333, 1),
+                                   (12000, 10000, 1)])
+def test_item_attention_layer_fp8(S, N, T, prec):
+    """Config E's fp8 path (MMPFN_PREC_BF16_F8 / _F8E5): P.V and the row sums on block-scaled fp8 MFMA, the
+    per-query scale from the first key tile, the partial tile's padded keys cancelled at P'(0)."""
+    q, k, v, Npad = _qkv_case(S, N, T, seed=S + N + prec)
+    got = _launch_layer(q, k, v, Npad, N, prec)
+    ref = _layer_ref(q, k, v, N, prec)
+    assert torch.isfinite(got).all()
+    err = (got.double() - ref).abs().max().item()
+    rms = ((got.double() - ref) ** 2).mean().sqrt().item()
+    print(f"fp8 attention ({'e4m3' if prec == 3 else 'e5m2'} P) S={S} N={N} T={T}: max {err:.3e} rms {rms:.3e}")
+    assert err < ATTN_TOL[prec]
+
+
+@pytest.mark.parametrize("prec", [1, 0, 3, 4])
 def test_item_attention_overflow_backstop(prec):
     """Scores that jump far past the first key tile's max (p would overflow the fixed
     softmax reference) take the exact two-pass recompute and still match."""
@@ -258,7 +279,7 @@ def test_item_attention_overflow_backstop(prec):
     assert (got.double() - ref).abs().max().item() < ATTN_TOL[prec]
 
 
-@pytest.mark.parametrize("prec", [1, 0])
+@pytest.mark.parametrize("prec", [1, 0, 3, 4])
 @pytest.mark.parametrize("kscale", [-5.0, 7.0])
 def test_item_attention_reference_rerun(kscale, prec):
     """Row sums outside [2^-60, 2^100) under the reference-free first pass (every score ~82 log2
@@ -273,12 +294,13 @@ def test_item_attention_reference_rerun(kscale, prec):
     assert torch.isfinite(got).all()
     err = (got.double() - ref).abs().max().item()
     print(f"rerun kscale {kscale} prec {prec}: {err:.3e}")
-    assert err < (2e-2 if prec == 1 else 1e-4)
+    assert err < (1e-4 if prec == 0 else ATTN_TOL[prec])
 
 
+@pytest.mark.parametrize("prec", [1, 3, 4])
 @pytest.mark.parametrize("N", [20, 65, 1838])
 @pytest.mark.parametrize("kscale", [-0.6, -0.7, -0.8, -0.9])
-def test_item_attention_padded_tile_small_sums(kscale, N):
+def test_item_attention_padded_tile_small_sums(kscale, N, prec):
     """The partial key tile runs in the pipelined loop with its padded keys at p = 1 and the row sums
     started at -npad (44, 63 or 18 padded keys here; N = 20: the partial tile is the only one); scores of
     about 16 kscale log2 units put the true sums around 2^-12 npad, on both sides of the threshold below
@@ -287,12 +309,12 @@ def test_item_attention_padded_tile_small_sums(kscale, N):
     q, k, v, Npad = _qkv_case(S, N, T, seed=N + 3)
     q[...] = q.sign() * 0.1 + 2.0
     k[...] = k * 0.02 + kscale
-    got = _launch_layer(q, k, v, Npad, N, 1)
-    ref = _layer_ref(q, k, v, N, 1)
+    got = _launch_layer(q, k, v, Npad, N, prec)
+    ref = _layer_ref(q, k, v, N, prec)
     assert torch.isfinite(got).all()
     err = (got.double() - ref).abs().max().item()
-    print(f"padded tile N={N} kscale {kscale}: {err:.3e}")
-    assert err < 2e-2
+    print(f"padded tile N={N} kscale {kscale} prec {prec}: {err:.3e}")
+    assert err < ATTN_TOL[prec]
 
 
 def _launch_cached(q, k0, v0, Npad, N):
@@ -488,10 +510,17 @@ def test_large_config_matches_oracle_on_device(name, S, N, F, n_cls, seed):
     model = make_model(cfg, sd)
     x = torch.from_numpy(synth_table(S, F, seed, nan_frac=0.01)).cuda()
     y = torch.from_numpy(synth_labels(S, n_cls, seed)[:N]).cuda()
+    from multimodalpfn_amd import _lib
+
+    f8 = {}
     with torch.inference_mode():
         f32 = model(None, x[:, None, :], None, y, single_eval_pos=N).squeeze(1).float().cpu().numpy()
         with torch.autocast("cuda"):
             b16 = model(None, x[:, None, :], None, y, single_eval_pos=N).squeeze(1).float().cpu().numpy()
+        if name[0] == "E":  # config E's fp8 path: P.V + row sums on block-scaled fp8 MFMA
+            for fmt, code in (("e4m3", _lib.PREC_BF16_F8), ("e5m2", _lib.PREC_BF16_F8E5)):
+                f8[fmt] = model(None, x[:, None, :], None, y, single_eval_pos=N,
+                                precision=code).squeeze(1).float().cpu().numpy()
     w = {k: v.cuda() for k, v in torch_sd(sd).items()}
     ref = oracle_forward(oracle_spec(cfg), w, x, None, y).cpu().numpy()
     del w
@@ -503,6 +532,13 @@ def test_large_config_matches_oracle_on_device(name, S, N, F, n_cls, seed):
     print(f"bf16 {name}: rel err {eb:.3e}; fp32 rel err {rel_err(f32, ref):.3e}")
     assert eb <= LARGE_BF16_TOL[name[0]], (name, eb)
     check_argmax(b16, ref, BF16_AGREE, f"bf16 {name}")
+    for fmt, out in f8.items():
+        e8 = rel_err(out, ref)
+        agree = float((out.argmax(1) == ref.argmax(1)).mean())
+        print(f"fp8 P.V ({fmt}) {name}: rel err {e8:.3e}, argmax agreement {agree:.4f}")
+        assert np.isfinite(out).all()
+        assert e8 <= F8_TOL, (name, fmt, e8)
+        check_argmax(out, ref, BF16_AGREE, f"fp8 {fmt} {name}")
 
 
 @pytest.mark.parametrize("prec", [0, 1])
