@@ -60,6 +60,12 @@ extern "C" {
                                   MFMA (V^T e4m3, P e4m3 under a per-query power-of-two scale): config E's fp8 path
                                   (multi_head_attention.py:693-729 in fp8); the train-KV cache keeps bf16 */
 #define MMPFN_PREC_BF16_F8E5 4 /* as MMPFN_PREC_BF16_F8 with P in e5m2 (wider range, 2 mantissa bits) */
+#define MMPFN_PREC_F16 5      /* the reference's fp16 autocast (utils.py:150-190, layer.py:60-62): the state X kept in
+                                  fp16 between kernels, every layer contraction on fp16 MFMA operands (the item
+                                  attention's P.V on bf16), fp32 accumulation / LayerNorm / softmax statistics;
+                                  tables of more than 64 tokens per row run MMPFN_PREC_BF16 */
+#define MMPFN_PREC_F16_F8 6   /* MMPFN_PREC_F16 with the fp8 P.V of MMPFN_PREC_BF16_F8 */
+#define MMPFN_PREC_F16_F8E5 7 /* MMPFN_PREC_F16 with the fp8 P.V of MMPFN_PREC_BF16_F8E5 */
 
 #define MMPFN_MIXER_NONE 0
 #define MMPFN_MIXER_MGM 1

@@ -26,6 +26,9 @@ PREC_BF16 = 1      # performance mode (the reference's fp16 autocast counterpart
 PREC_F32_MFMA = 2  # parity mode on fp32-input MFMA (exact fp32 fma chains, 1/16 of the bf16 rate)
 PREC_BF16_F8 = 3   # bf16 mode with the sample-axis attention's P.V on fp8 MFMA (P e4m3): config E's fp8 path
 PREC_BF16_F8E5 = 4  # the same with P in e5m2
+PREC_F16 = 5       # the reference's fp16 autocast: fp16 state between kernels, fp16 MFMA operands, fp32 statistics
+PREC_F16_F8 = 6    # PREC_F16 with the fp8 P.V (P e4m3)
+PREC_F16_F8E5 = 7  # PREC_F16 with the fp8 P.V (P e5m2)
 
 
 def f32_precision() -> int:
@@ -41,11 +44,22 @@ def precision_of_dtype(dtype) -> int:
 
     if dtype in (torch.float32, torch.float64):
         return f32_precision()
+    if dtype == torch.float16:
+        return PREC_F16
+    if dtype == torch.bfloat16:
+        return PREC_BF16
+    base = autocast_precision()
     if dtype == torch.float8_e4m3fn:
-        return PREC_BF16_F8
+        return PREC_F16_F8 if base == PREC_F16 else PREC_BF16_F8
     if dtype == torch.float8_e5m2:
-        return PREC_BF16_F8E5
-    return PREC_BF16
+        return PREC_F16_F8E5 if base == PREC_F16 else PREC_BF16_F8E5
+    return base
+
+
+def autocast_precision() -> int:
+    """Engine code of the reference's GPU default (``inference_precision="auto"``: fp16 autocast): PREC_BF16
+    unless ``MMPFN_AUTOCAST=f16`` selects PREC_F16."""
+    return PREC_F16 if os.environ.get("MMPFN_AUTOCAST", "bf16").lower() == "f16" else PREC_BF16
 
 MIXER_NONE, MIXER_MGM, MIXER_MGM_CAP, MIXER_MOE = 0, 1, 2, 3
 MIXER_CODES = {"MGM": MIXER_MGM, "MGM+CAP": MIXER_MGM_CAP, "MoE": MIXER_MOE, None: MIXER_NONE}

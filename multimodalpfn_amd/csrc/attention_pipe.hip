@@ -29,6 +29,9 @@
 // room for the fixed reference 0, so each query gets a power-of-two conversion scale from its first key
 // tile's max (the first tile's max lands at 2^ETOP); a later score beyond the format's range converts to
 // NaN / inf, which the row-sum check catches, and the wave re-runs on the exact bf16 path.
+//
+// QF16 (PREC_F16): Q / K and the output O in fp16, so S = K Q^T runs on v_mfma_f32_32x32x16_f16 (same
+// rate); V^T and P stay bf16 (P = exp2(s) under the fixed reference needs bf16's exponent range).
 #include <type_traits>
 
 #include "common.h"
@@ -73,13 +76,17 @@ constexpr int SG_VALU = 0x2, SG_MFMA = 0x8, SG_VMEM_READ = 0x20, SG_DS_READ = 0x
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
 // exact two-pass softmax for one query per lane, K / V^T straight from global memory (backstop)
-__device__ __attribute__((noinline)) void p4_exact_rows(const Attn2Args& p, const bf16* Kg, const bf16* Vg,
-                                                        const bf16* qrow, bf16* orow, bool valid, float c) {
+template <typename QT>
+__device__ __attribute__((noinline)) void p4_exact_rows(const Attn2Args& p, const QT* Kg, const bf16* Vg,
+                                                        const QT* qrow, QT* orow, bool valid, float c) {
   float q[32], o[32];
 #pragma unroll
   for (int d = 0; d < 32; ++d) q[d] = (float)qrow[d] * c, o[d] = 0.f;
@@ -103,12 +110,15 @@ __device__ __attribute__((noinline)) void p4_exact_rows(const Attn2Args& p, cons
   if (valid) {
     const float inv = 1.0f / l;
 #pragma unroll
-    for (int d = 0; d < 32; ++d) orow[d] = (bf16)(o[d] * inv);
+    for (int d = 0; d < 32; ++d) orow[d] = (QT)(o[d] * inv);
   }
 }
 
-template <int F8>
+template <int F8, bool QF16>
 __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
+  typedef typename Op16<QF16>::t QT;    // Q, K and O elements
+  typedef typename Op16<QF16>::x8 Q8;
+  typedef typename Op16<QF16>::x4 Q4;
   // LDS slot: K [64][32] bf16 in 80-B rows | V^T [32][64] in 144-B rows (bf16) or 80-B rows (e4m3)
   constexpr int VROW = F8 ? 80 : 144;
   constexpr int P4_SLOT_BYTES = 64 * 80 + 32 * VROW;
@@ -139,7 +149,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   const bool active = jw < cnt;  // wave-uniform; an idle wave only stages its share of every tile
 
   const int64_t kvoff = (int64_t)b * p.kv_bstride + (int64_t)g * p.Npad * 32;
-  const bf16* Kg = p.k + kvoff;
+  const QT* Kg = (const QT*)p.k + kvoff;
   const bf16* Vg = p.vt + kvoff;
   const unsigned char* Vg8 = p.vt8 + kvoff;  // F8: e4m3 V^T, same element layout
   const float c = kLog2e * 0.17677669529663687f;  // log2(e)/sqrt(32)
@@ -162,19 +172,19 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     }
     return q;
   };
-  bf16x8 qf[P4_NCH][2];
+  Q8 qf[P4_NCH][2];
 #pragma unroll
   for (int qb = 0; qb < P4_NCH; ++qb) {
     const QRow q = qrow_of(qb);
-    const bf16* qrow = p.q + (((int64_t)b * p.H + q.h) * p.S + q.s) * 32;
+    const QT* qrow = (const QT*)p.q + (((int64_t)b * p.H + q.h) * p.S + q.s) * 32;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 raw = *(const bf16x8*)(qrow + 16 * ks + 8 * hh);
+      const Q8 raw = *(const Q8*)(qrow + 16 * ks + 8 * hh);
       if (p.q_prescaled) {
         qf[qb][ks] = raw;
       } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (bf16)((float)raw[e] * c);
+        for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (QT)((float)raw[e] * c);
       }
     }
   }
@@ -210,11 +220,11 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       kro[u][i] = kb + 32 * u * KROW + 32 * i;
       vro[u][i] = vb + 64 * u + 32 * i;
     }
-  auto readk = [&](bf16x8(&kf)[2][2], const unsigned char* slot) __attribute__((always_inline)) {
+  auto readk = [&](Q8(&kf)[2][2], const unsigned char* slot) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) kf[u][ks] = *(const bf16x8*)(slot + kro[u][ks]);
+      for (int ks = 0; ks < 2; ++ks) kf[u][ks] = *(const Q8*)(slot + kro[u][ks]);
   };
   using VFrag = std::conditional_t<F8 != 0, i32x8, bf16x8[2][2]>;  // V^T fragments of one tile
   using PFrag = std::conditional_t<F8 != 0, i32x8, bf16x8[2][2]>;  // P^T fragments of one (tile, chain)
@@ -270,12 +280,12 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     __builtin_amdgcn_sched_barrier(0);
   };
   // direct fragment loads (the non-pipelined tile below)
-  auto loadk = [&](bf16x8(&kf)[2][2], int t) __attribute__((always_inline)) {
-    const bf16* s = Kg + ((int64_t)t * P4_KT + pkr) * 32 + 8 * hh;
+  auto loadk = [&](Q8(&kf)[2][2], int t) __attribute__((always_inline)) {
+    const QT* s = Kg + ((int64_t)t * P4_KT + pkr) * 32 + 8 * hh;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) kf[u][ks] = *(const bf16x8*)(s + u * 32 * 32 + 16 * ks);
+      for (int ks = 0; ks < 2; ++ks) kf[u][ks] = *(const Q8*)(s + u * 32 * 32 + 16 * ks);
   };
   auto loadv = [&](bf16x8(&vf)[2][2], int t) __attribute__((always_inline)) {
     const bf16* s = Vg + (int64_t)r * p.Npad + t * P4_KT + 8 * hh;
@@ -315,7 +325,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   for (int qb = 0; qb < P4_NCH; ++qb) lacc[qb] = f32x4{-padsum, -padsum, -padsum, -padsum};
 
   const f32x16 zero16 = {};
-  auto smm = [&](f32x16(&s)[2], const bf16x8(&kf)[2][2], int qb) __attribute__((always_inline)) {
+  auto smm = [&](f32x16(&s)[2], const Q8(&kf)[2][2], int qb) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       s[u] = mfma32(kf[u][0], qf[qb][0], zero16);
@@ -460,7 +470,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   //   step (t, 1): S(t+1, chain 0) | exp S(t, chain 1) | P.V(t, chain 0); then the tile's barrier
   // kf(t) in register set t % 2, vf(t) in set (t + 1) % 2
   if (ntiles > 0) {
-    bf16x8 kf[2][2][2];
+    Q8 kf[2][2][2];
     VFrag vf[2];
     f32x16 sa[2], sb[2];
     PFrag pa, pz;
@@ -573,7 +583,8 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   float mref[P4_NCH] = {0.f, 0.f};
   auto tile1 = [&](int t, bool first, bool ref) {
     const int k0 = t * P4_KT;
-    bf16x8 kf[2][2], vf[2][2];
+    Q8 kf[2][2];
+    bf16x8 vf[2][2];
     loadk(kf, t);
     loadv(vf, t);
     const bool mask = k0 + P4_KT > p.nk;
@@ -643,9 +654,9 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   for (int qb = 0; qb < P4_NCH; ++qb) {
     const float ls = rowsum(qb);
     const QRow q = qrow_of(qb);
-    bf16* orow = p.o + ((int64_t)b * p.S + q.s) * (p.H * 32) + q.h * 32;
+    QT* orow = (QT*)p.o + ((int64_t)b * p.S + q.s) * (p.H * 32) + q.h * 32;
     if (__any((__float_as_uint(ls) & 0x7fffffffu) >= 0x71800000u)) {
-      const bf16* qrow = p.q + (((int64_t)b * p.H + q.h) * p.S + q.s) * 32;
+      const QT* qrow = (const QT*)p.q + (((int64_t)b * p.H + q.h) * p.S + q.s) * 32;
       p4_exact_rows(p, Kg, Vg, qrow, orow, q.ok && hh == 0, p.q_prescaled ? 1.0f : c);
       continue;
     }
@@ -654,9 +665,9 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     u32x2 w[4];
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq) {
-      bf16x4 v;
+      Q4 v;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (bf16)(o[qb][4 * gq + e] * inv);
+      for (int e = 0; e < 4; ++e) v[e] = (QT)(o[qb][4 * gq + e] * inv);
       w[gq] = __builtin_bit_cast(u32x2, v);
     }
 #pragma unroll
@@ -671,17 +682,24 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
 
 }  // namespace
 
-hipError_t launch_attn_pipe(const Attn2Args& a, hipStream_t st) {
+namespace {
+template <bool QF16>
+hipError_t launch_pipe(const Attn2Args& a, hipStream_t st) {
   if (a.f8 == 1) {
     if (!a.vt8) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(attn_pipe_kernel<1>, dim3(a.nblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_pipe_kernel<1, QF16>), dim3(a.nblocks), dim3(256), 0, st, a);
   } else if (a.f8 == 2) {
     if (!a.vt8) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(attn_pipe_kernel<2>, dim3(a.nblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_pipe_kernel<2, QF16>), dim3(a.nblocks), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL(attn_pipe_kernel<0>, dim3(a.nblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_pipe_kernel<0, QF16>), dim3(a.nblocks), dim3(256), 0, st, a);
   }
   return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_attn_pipe(const Attn2Args& a, hipStream_t st) {
+  return a.qk_f16 ? launch_pipe<true>(a, st) : launch_pipe<false>(a, st);
 }
 
 namespace {

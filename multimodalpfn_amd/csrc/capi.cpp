@@ -6,7 +6,8 @@
 //   -> nlayers x [feature attn | item attn | MLP] (layer.py:272-457)
 //   -> decoder on the test rows of the target token.
 // State layout in HBM: X[T][S][E] fp32 (token-major), so every token column of the
-// sample-axis attention is a contiguous [S][E] slab.
+// sample-axis attention is a contiguous [S][E] slab; fp16 under PREC_F16 (the encoders and the
+// decoder run in fp32 and convert at the seams).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -36,6 +37,10 @@ struct LayerW {  // packed per layer, [N][K] row-major
   DevBuf feat_qkv, feat_out, item_qkv, item_qtest, item_out, mlp1, mlp2;  // fp32
   DevBuf feat_qkv_h, feat_out_h, item_qkv_h, item_qtest_h, item_out_h, mlp1_h, mlp2_h;  // bf16
   DevBuf feat_pack_h;  // bf16 LDS images of the feature-attention weights (featrow.hip)
+  // PREC_F16 (fp16): feature-attention images (out-projection rows in f16_row_perm order), item q|k|v and
+  // test q (Q rows prescaled like the bf16 copies), item out-projection and MLP W2 with f16_row_perm rows,
+  // MLP W1 natural
+  DevBuf feat_pack_f, item_qkv_f, item_qtest_f, item_out_f, mlp1_f, mlp2_f;
 };
 
 }  // namespace
@@ -77,7 +82,8 @@ struct mmpfn_ctx {
   // workspace of the selected lane (per-member forward state)
   DevBuf ws_X, ws_O, ws_big, ws_pe, ws_slots, ws_scr, ws_flag;
   DevBuf mx[8];
-  DevBuf tap_v8;  // e4m3 V^T of the fp8 attention tap
+  DevBuf tap_v8;   // e4m3 V^T of the fp8 attention tap
+  DevBuf tap_x16;  // PREC_F16 taps: the caller's fp32 state as fp16
   // current forward geometry (M members of equal geometry stacked as [M][T][S][E]); f8: the fp8 P.V
   // variant of the item attention (f8_of of the forward's precision code; prec holds its base_prec)
   int S = 0, T = 0, N = 0, G = 0, C = 0, Npad = 0, prec = 0, M = 1, f8 = 0;
@@ -148,6 +154,16 @@ int ensure_flag(mmpfn_ctx* ctx, DevBuf& b, hipStream_t st) {
   if (b.p) return MMPFN_OK;
   RC_(ensure(ctx, b, 256));
   HIPCHK(hipMemsetAsync(b.p, 0, 256, st));
+  return MMPFN_OK;
+}
+
+// fp16 copy (PREC_F16 weights)
+int upload_f16(mmpfn_ctx* ctx, DevBuf& b, const std::vector<float>& v) {
+  std::vector<uint16_t> h(v.size());
+  for (size_t i = 0; i < v.size(); ++i) h[i] = f2h(v[i]);
+  int rc = ensure(ctx, b, h.size() * 2);
+  if (rc) return rc;
+  HIPCHK(hipMemcpy(b.p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
   return MMPFN_OK;
 }
 
@@ -226,9 +242,15 @@ int finalize(mmpfn_ctx* ctx) {
     GETW(m2, p + "mlp.linear2.weight", (size_t)E * Fh);
     if ((rc = up2(ctx, L.feat_qkv, L.feat_qkv_h, *fq))) return rc;
     if ((rc = up2(ctx, L.feat_out, L.feat_out_h, transpose_out(*fo, HD, E)))) return rc;
-    if (E == 192 && d.nhead == 6)
+    if (E == 192 && d.nhead == 6) {
       if ((rc = upload(ctx, L.feat_pack_h, pack_feat_rows(*fq, transpose_out(*fo, HD, E), d.nhead, E), true)))
         return rc;
+      if ((rc = upload_f16(ctx, L.feat_pack_f, pack_feat_rows(*fq, transpose_out(*fo, HD, E), d.nhead, E, true))))
+        return rc;
+      if ((rc = upload_f16(ctx, L.item_out_f, permute_rows_f16(transpose_out(*io, HD, E), E, HD)))) return rc;
+      if ((rc = upload_f16(ctx, L.mlp1_f, *m1))) return rc;
+      if ((rc = upload_f16(ctx, L.mlp2_f, permute_rows_f16(pack_mlp2_perm(*m2, E, Fh), E, Fh)))) return rc;
+    }
     if ((rc = up2(ctx, L.item_out, L.item_out_h, transpose_out(*io, HD, E)))) return rc;
     if ((rc = upload(ctx, L.mlp1, *m1, false))) return rc;
     if ((rc = upsplit(ctx, L.mlp1, *m1))) return rc;
@@ -260,6 +282,8 @@ int finalize(mmpfn_ctx* ctx) {
     for (float& w : wtest) w *= qsc;
     if ((rc = upload(ctx, L.item_qkv_h, wtrain, true))) return rc;
     if ((rc = upload(ctx, L.item_qtest_h, wtest, true))) return rc;
+    if ((rc = upload_f16(ctx, L.item_qkv_f, wtrain))) return rc;
+    if ((rc = upload_f16(ctx, L.item_qtest_f, wtest))) return rc;
   }
   int rc;
   {
@@ -465,6 +489,8 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
   const int E = d.emsize, fpg = d.features_per_group;
   const int G = x ? (F + fpg - 1) / fpg : 0;
   const int T = G + C + 1;
+  // PREC_F16's layer kernels hold a row's tokens as up to four 16-token tiles; wider tables run PREC_BF16
+  if (prec == PREC_F16 && (T > 64 || E != 192 || d.nhead != 6)) prec = PREC_BF16;
   const int Npad = (N + 63) / 64 * 64;
   const size_t R = (size_t)S * T;
   hipStream_t st = ctx->stream;
@@ -490,7 +516,9 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
       return fail(ctx, MMPFN_ERR_INVALID, "batched members must share S, N, F, C and precision");
     flag = (int*)ctx->ws_flag.p;
   }
-  float* X = (float*)ctx->ws_X.p + (size_t)m * R * E;
+  // PREC_F16: the encoders write fp32 into the attention-output workspace, converted into the fp16 state
+  const bool h = prec == PREC_F16;
+  float* X = h ? (float*)ctx->ws_O.p + (size_t)m * R * E : (float*)ctx->ws_X.p + (size_t)m * R * E;
   if (G) {
     HIPCHK(launch_encode_x(x, S, F, N, G, fpg, d.encoder_features, d.outlier_sigma, (SlotParams*)ctx->ws_slots.p,
                            (const float*)ctx->enc_w.p, (const float*)ctx->ws_pe.p, X, E, flag, st));
@@ -501,6 +529,7 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
   }
   HIPCHK(launch_encode_y(y, N, S, uniq, U, (const float*)ctx->y_w.p, (const float*)ctx->y_b.p,
                          X + (size_t)(T - 1) * S * E, E, (float*)ctx->ws_scr.p, flag, st));
+  if (h) HIPCHK(launch_f32_to_f16(X, 0, (uint16_t*)ctx->ws_X.p + (size_t)m * R * E, 0, (int64_t)R * E, 1, st));
   ctx->embedded = true;
   return MMPFN_OK;
 }
@@ -518,6 +547,7 @@ int embed_cached(mmpfn_ctx* ctx, const mmpfn_cache* cc, const float* x, int S, i
   const size_t R = (size_t)S * T;
   hipStream_t st = ctx->stream;
   ctx->S = S, ctx->T = T, ctx->N = 0, ctx->G = G, ctx->C = C, ctx->Npad = 0, ctx->prec = prec, ctx->M = 1;
+  const bool h = prec == PREC_F16;
   ctx->f8 = 0;  // the cache keeps bf16 V^T: its test rows run the bf16 P.V
   RC(ensure(ctx, ctx->ws_X, R * E * 4));
   RC(ensure(ctx, ctx->ws_O, R * E * 4));
@@ -525,7 +555,7 @@ int embed_cached(mmpfn_ctx* ctx, const mmpfn_cache* cc, const float* x, int S, i
   RC(ensure(ctx, ctx->ws_big, (R * E + (size_t)2 * S * Tpad * E) * 4));
   RC(ensure_flag(ctx, ctx->ws_flag, st));
   int* flag = (int*)ctx->ws_flag.p;
-  float* X = (float*)ctx->ws_X.p;
+  float* X = h ? (float*)ctx->ws_O.p : (float*)ctx->ws_X.p;
   const float* pe = (const float*)cc->pe.p;
   if (G)
     HIPCHK(launch_encode_x(x, S, F, 0, G, fpg, d.encoder_features, d.outlier_sigma, (SlotParams*)cc->slots.p,
@@ -534,6 +564,7 @@ int embed_cached(mmpfn_ctx* ctx, const mmpfn_cache* cc, const float* x, int S, i
   HIPCHK(launch_encode_y(nullptr, 0, S, (const float*)cc->uniq.p, cc->U, (const float*)ctx->y_w.p,
                          (const float*)ctx->y_b.p, X + (size_t)(T - 1) * S * E, E, (float*)cc->ymean.p, flag, st,
                          false));
+  if (h) HIPCHK(launch_f32_to_f16(X, 0, ctx->ws_X.p, 0, (int64_t)R * E, 1, st));
   ctx->embedded = true;
   return MMPFN_OK;
 }
@@ -545,7 +576,7 @@ void cache_release(mmpfn_cache* cc) {
 }
 
 // ---- attention between features (layer.py:332-339): X [M][T][S][E] <- LN(X + FeatAttn(X)), batch = row s
-int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int S, int T, int M, int prec) {
+int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, void* Xv, int S, int T, int M, int prec) {
   const mmpfn_model_desc& d = ctx->d;
   const int E = d.emsize, H = d.nhead;
   const int64_t R = (int64_t)S * T;
@@ -554,6 +585,12 @@ int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int S, int T, in
   hipStream_t st = ctx->stream;
   void* O = ctx->ws_O.p;
   unsigned char* big = (unsigned char*)ctx->ws_big.p;
+  if (prec == PREC_F16) {  // fp16 state: the row-resident kernel only (embed keeps F16 to T <= 64)
+    if (!L.feat_pack_f.p || T > 64) return fail(ctx, MMPFN_ERR_INVALID, "PREC_F16 needs E = 192, 6 heads, T <= 64");
+    HIPCHK(launch_feat_rows(Xv, L.feat_pack_f.p, S, T, M, E, H, d.ln_eps, st, true));
+    return MMPFN_OK;
+  }
+  float* Xall = (float*)Xv;
   if (bf && L.feat_pack_h.p && T <= 64) {
     // one wave per row (all M members' rows in one launch), the whole sublayer in registers (featrow.hip)
     HIPCHK(launch_feat_rows(Xall, L.feat_pack_h.p, S, T, M, E, H, d.ln_eps, st));
@@ -604,13 +641,18 @@ int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int S, int T, in
 //      (member*T + t)*N + n -> memory row (member*T + t)*S + n, attention batch member*T + t.
 //      fuse_out: the out-projection + residual + LN is left to the MLP kernel's prologue (the
 //      attention output stays in ws_O); otherwise X <- LN(X + O Wout^T) here.
-int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int Npad, int M, int prec,
+int item_sublayer(mmpfn_ctx* ctx, int l, void* Xv, int S, int T, int N, int Npad, int M, int prec,
                   bool fuse_out, int f8 = 0) {
   const mmpfn_model_desc& d = ctx->d;
   const LayerW& L = ctx->layers[l];
   const int E = d.emsize, H = d.nhead, Q = S - N;
   const int64_t RM = (int64_t)S * T * M;  // tokens of the batch
   const int TM = T * M;                   // token columns of the batch (attention batches)
+  float* Xall = (float*)Xv;
+  // PREC_F16 runs the bf16 mode's kernels in their F16 forms (fp16 X, Q, K, O; bf16 V^T)
+  const bool h16 = prec == PREC_F16;
+  if (h16 && E != 192) return fail(ctx, MMPFN_ERR_INVALID, "PREC_F16 needs E = 192");
+  if (h16) prec = PREC_BF16;
   const bool bf = prec == PREC_BF16;
   const int eb = bf ? 2 : 4;
   hipStream_t st = ctx->stream;
@@ -625,7 +667,8 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
     const unsigned char* Kc = (const unsigned char*)cc->kv.p + (size_t)l * 2 * kvl;
     const unsigned char* Vc = Kc + kvl;
     if (bf && E == 192) {
-      HIPCHK(launch_rowgemm_qkv(Xall, S, S, 1, 0, L.item_qtest_h.p, TM * S, E, Qi, Ki, Vi, S, Npad, H, st));
+      HIPCHK(launch_rowgemm_qkv(Xv, S, S, 1, 0, h16 ? L.item_qtest_f.p : L.item_qtest_h.p, TM * S, E, Qi, Ki, Vi, S,
+                                Npad, H, st, h16));
     } else if (proj3_ok(ctx, prec)) {
       const Proj3Set ps = p3set(ctx, L.item_qtest, Xall, S, S, 1, 0, (int64_t)TM * S, E);
       HIPCHK(launch_proj3_qkv(&ps, 1, Qi, Ki, Vi, S, Npad, H, st));
@@ -639,14 +682,16 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
     }
     const int64_t cstride = (int64_t)cc->Npad * 32;
     if (bf)
-      HIPCHK(launch_attn_layer(Qi, Kc, Vc, O, S, TM, H, cc->Npad, cc->N, 0, 0, 0, S, 0, st, cstride, true));
+      HIPCHK(launch_attn_layer(Qi, Kc, Vc, O, S, TM, H, cc->Npad, cc->N, 0, 0, 0, S, 0, st, cstride, true, nullptr, 0,
+                               h16));
     else
       HIPCHK(launch_attn_item(Qi, Kc, Vc, O, S, TM, H, cc->Npad, 0, S, cc->N, 0, prec, st, cstride));
   } else {
     if (bf && E == 192) {  // row-resident projections straight into the attention layouts
       // train rows q|k|v and test rows q in one launch (test-row blocks last)
-      HIPCHK(launch_rowgemm_qkv_pair(Xall, N, 0, L.item_qkv_h.p, TM * N, 3 * E, Q, N, L.item_qtest_h.p, TM * Q, E, S,
-                                     Qi, Ki, Vi, S, Npad, H, st));
+      HIPCHK(launch_rowgemm_qkv_pair(Xv, N, 0, h16 ? L.item_qkv_f.p : L.item_qkv_h.p, TM * N, 3 * E, Q, N,
+                                     h16 ? L.item_qtest_f.p : L.item_qtest_h.p, TM * Q, E, S, Qi, Ki, Vi, S, Npad, H, st,
+                                     h16));
     } else if (proj3_ok(ctx, prec)) {  // train rows q|k|v and test rows q in one launch
       const Proj3Set ps[2] = {p3set(ctx, L.item_qkv, Xall, N, S, 1, 0, (int64_t)TM * N, 3 * E),
                               p3set(ctx, L.item_qtest, Xall, Q > 0 ? Q : 1, S, 1, N, (int64_t)TM * Q, E)};
@@ -693,7 +738,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
         HIPCHK(launch_vt_fp8(Vi, V8, (int64_t)TM * H * Npad * 32, st));
       }
       if (ev) HIPCHK(hipEventRecord(ev[0], st));
-      HIPCHK(launch_attn_layer(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st, 0, true, V8, f8));
+      HIPCHK(launch_attn_layer(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st, 0, true, V8, f8, h16));
       if (ev) HIPCHK(hipEventRecord(ev[1], st));
     } else if (prec == PREC_F32) {  // parity mode: split-bf16 products, train and test rows in one launch
       HIPCHK(launch_attn_item3(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st));
@@ -704,7 +749,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
   }
   if (fuse_out) return MMPFN_OK;
   if (bf && E == 192) {
-    HIPCHK(launch_rowgemm_resln(O, L.item_out_h.p, RM, Xall, d.ln_eps, st));
+    HIPCHK(launch_rowgemm_resln(O, h16 ? L.item_out_f.p : L.item_out_h.p, RM, Xv, d.ln_eps, st, h16));
   } else if (proj3_ok(ctx, prec)) {
     HIPCHK(p3_resln(ctx, L.item_out, O, RM, Xall, st));
   } else {
@@ -717,12 +762,19 @@ int item_sublayer(mmpfn_ctx* ctx, int l, float* Xall, int S, int T, int N, int N
 }
 
 // the bf16 MLP kernel runs the item-attention out-projection as its prologue
-bool mlp_fuses_out(const mmpfn_model_desc& d, int prec) { return prec == PREC_BF16 && d.emsize == 192 && d.nhid % 32 == 0; }
+bool mlp_fuses_out(const mmpfn_model_desc& d, int prec) {
+  return prec16(prec) && d.emsize == 192 && d.nhid % 32 == 0;
+}
 
 // ---- MLP (mlp.py:93-104) + residual + LN over RM tokens; O non-null: the fused out-projection first
-int mlp_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int64_t RM, int prec, const void* O) {
+int mlp_sublayer(mmpfn_ctx* ctx, const LayerW& L, void* Xv, int64_t RM, int prec, const void* O) {
   const mmpfn_model_desc& d = ctx->d;
-  if (mlp_fuses_out(d, prec)) {  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders
+  float* Xall = (float*)Xv;
+  if (prec == PREC_F16) {  // fp16 copies: W1 natural, W2 / Wout rows in f16_row_perm order
+    if (!mlp_fuses_out(d, prec) || !L.mlp1_f.p) return fail(ctx, MMPFN_ERR_INVALID, "PREC_F16 needs E = 192");
+    HIPCHK(launch_mlp_rows(Xv, L.mlp1_f.p, L.mlp2_f.p, RM, d.emsize, d.nhid, d.ln_eps, ctx->stream, O,
+                           O ? L.item_out_f.p : nullptr, true));
+  } else if (mlp_fuses_out(d, prec)) {  // W1 / W2 bf16 copies in mlp_rows_kernel's K orders
     HIPCHK(launch_mlp_rows(Xall, L.mlp1_h.p, L.mlp2_h.p, RM, d.emsize, d.nhid, d.ln_eps, ctx->stream, O,
                            O ? L.item_out_h.p : nullptr));
   } else if (prec == PREC_F32) {  // parity mode: mlp_x3_kernel on split-bf16 products (W1 / W2 hi | lo planes)
@@ -738,7 +790,7 @@ int mlp_sublayer(mmpfn_ctx* ctx, const LayerW& L, float* Xall, int64_t RM, int p
 int run_layer(mmpfn_ctx* ctx, int l) {
   const LayerW& L = ctx->layers[l];
   const int S = ctx->S, T = ctx->T, N = ctx->N, Npad = ctx->Npad, prec = ctx->prec, M = ctx->M;
-  float* Xall = (float*)ctx->ws_X.p;
+  void* Xall = ctx->ws_X.p;
   const bool fuse = mlp_fuses_out(ctx->d, prec);
   RC(feat_sublayer(ctx, L, Xall, S, T, M, prec));
   RC(item_sublayer(ctx, l, Xall, S, T, N, Npad, M, prec, fuse, ctx->f8));
@@ -760,11 +812,19 @@ int tap_workspace(mmpfn_ctx* ctx, int S, int T, int Npad) {
 int decode(mmpfn_ctx* ctx, float* logits, int M = 1) {
   const mmpfn_model_desc& d = ctx->d;
   const int E = d.emsize, S = ctx->S, T = ctx->T, N = ctx->N, Q = S - N;
-  const float* Xl = (const float*)ctx->ws_X.p + ((size_t)(T - 1) * S + N) * E;
+  const size_t off = ((size_t)(T - 1) * S + N) * E;
+  const float* Xl = (const float*)ctx->ws_X.p + off;
+  int64_t xm = (int64_t)S * T * E;
+  if (ctx->prec == PREC_F16) {  // the target token's test rows of every member to fp32 (the big workspace is free)
+    RC(ensure(ctx, ctx->ws_big, (size_t)M * Q * E * 4));
+    HIPCHK(launch_f16_to_f32((const uint16_t*)ctx->ws_X.p + off, xm, (float*)ctx->ws_big.p, (int64_t)Q * E,
+                             (int64_t)Q * E, M, ctx->stream));
+    Xl = (const float*)ctx->ws_big.p, xm = (int64_t)Q * E;
+  }
   RC(ensure(ctx, ctx->ws_O, (size_t)M * (d.nhid / 32 + 1) * Q * d.n_out * sizeof(float)));
   HIPCHK(launch_decoder(Xl, Q, (const float*)ctx->dec_w1.p, (const float*)ctx->dec_b1.p, d.nhid,
                         (const float*)ctx->dec_w2.p, (const float*)ctx->dec_b2.p, d.n_out, logits, E, ctx->stream, M,
-                        (int64_t)S * T * E, (int64_t)Q * d.n_out, (float*)ctx->ws_O.p));
+                        xm, (int64_t)Q * d.n_out, (float*)ctx->ws_O.p));
   return MMPFN_OK;
 }
 
@@ -891,6 +951,20 @@ int mixer(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, i
   return fail(ctx, MMPFN_ERR_INVALID, "model has no mixer");
 }
 
+// a tap on the caller's fp32 state: PREC_F16 runs it on an fp16 copy and converts the result back
+// (f16_ok false: the sublayer has no fp16 form at this shape and runs PREC_BF16, as the forward does)
+template <typename F>
+int state_tap(mmpfn_ctx* ctx, float* X, int64_t n, int precision, bool f16_ok, F&& run) {
+  int bp = base_prec(precision);
+  if (bp == PREC_F16 && !f16_ok) bp = PREC_BF16;
+  if (bp != PREC_F16) return run((void*)X, bp);
+  RC(ensure(ctx, ctx->tap_x16, (size_t)n * 2));
+  HIPCHK(launch_f32_to_f16(X, 0, ctx->tap_x16.p, 0, n, 1, ctx->stream));
+  RC(run(ctx->tap_x16.p, bp));
+  HIPCHK(launch_f16_to_f32(ctx->tap_x16.p, 0, X, 0, n, 1, ctx->stream));
+  return MMPFN_OK;
+}
+
 }  // namespace
 
 // ===================================================================== C ABI
@@ -921,7 +995,8 @@ void mmpfn_destroy(mmpfn_ctx* ctx) {
   for (auto& L : ctx->layers) {
     for (DevBuf* b : {&L.feat_qkv, &L.feat_out, &L.item_qkv, &L.item_qtest, &L.item_out, &L.mlp1, &L.mlp2,
                       &L.feat_qkv_h, &L.feat_out_h, &L.item_qkv_h, &L.item_qtest_h, &L.item_out_h, &L.mlp1_h,
-                      &L.mlp2_h, &L.feat_pack_h})
+                      &L.mlp2_h, &L.feat_pack_h, &L.feat_pack_f, &L.item_qkv_f, &L.item_qtest_f, &L.item_out_f,
+                      &L.mlp1_f, &L.mlp2_f})
       fr(*b);
   }
   for (DevBuf* b : {&ctx->enc_w, &ctx->y_w, &ctx->y_b, &ctx->pe_w, &ctx->pe_b, &ctx->dec_w1, &ctx->dec_b1,
@@ -931,7 +1006,7 @@ void mmpfn_destroy(mmpfn_ctx* ctx) {
                     &ctx->cap_f3, &ctx->cap_f3_h, &ctx->cap_f3_b, &ctx->cap_ng, &ctx->cap_nb, &ctx->moe_w1,
                     &ctx->moe_w1_h, &ctx->moe_b1, &ctx->moe_w2, &ctx->moe_w2_h, &ctx->moe_b2, &ctx->moe_gw,
                     &ctx->moe_gb, &ctx->ws_X, &ctx->ws_O, &ctx->ws_big, &ctx->ws_pe, &ctx->ws_slots, &ctx->ws_scr,
-                    &ctx->ws_flag, &ctx->tap_v8})
+                    &ctx->ws_flag, &ctx->tap_v8, &ctx->tap_x16})
     fr(*b);
   for (auto& b : ctx->mx) fr(b);
   for (auto& kv : ctx->split) fr(kv.second);
@@ -1013,7 +1088,9 @@ int mmpfn_mixer_forward(mmpfn_ctx* ctx, const float* image, int S, int n_mod, fl
   if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
   if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
-  return mixer(ctx, image, S, n_mod, tokens, base_prec(precision));
+  // (PREC_F16 projects the modality tokens in the bf16 mode: they enter the state through the fp32 encoders)
+  const int bp = base_prec(precision);
+  return mixer(ctx, image, S, n_mod, tokens, bp == PREC_F16 ? PREC_BF16 : bp);
 }
 
 int mmpfn_embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int C, const float* y, int N,
@@ -1066,6 +1143,10 @@ int mmpfn_copy_state(mmpfn_ctx* ctx, float* out, int64_t cap) {
   if (!ctx || !out) return MMPFN_ERR_INVALID;
   const int S = ctx->S, T = ctx->T, E = ctx->d.emsize;
   if (cap < (int64_t)S * T * E) return fail(ctx, MMPFN_ERR_INVALID, "state buffer too small");
+  if (ctx->prec == PREC_F16) {
+    HIPCHK(launch_state_f16_to_f32(ctx->ws_X.p, out, S, T, E, ctx->stream));
+    return MMPFN_OK;
+  }
   // [T][S][E] -> [S][T][E]
   for (int t = 0; t < T; ++t)
     HIPCHK(hipMemcpy2DAsync(out + (size_t)t * E, (size_t)T * E * 4, (const float*)ctx->ws_X.p + (size_t)t * S * E,
@@ -1125,9 +1206,9 @@ int mmpfn_cache_build(mmpfn_ctx* ctx, const float* x, int N, int F, const float*
   precision = base_prec(precision);  // the cache keeps bf16 K / V^T: fp8 P.V codes build a bf16 cache
   RC(embed(ctx, x, N, F, tokens, C, y_train, N, uniq, U, pos_rand, precision));
   const mmpfn_model_desc& d = ctx->d;
-  const int E = d.emsize, fpg = d.features_per_group, eb = precision == PREC_BF16 ? 2 : 4;
+  const int E = d.emsize, fpg = d.features_per_group, eb = prec16(ctx->prec) ? 2 : 4;
   mmpfn_cache* cc = new mmpfn_cache;
-  cc->N = N, cc->F = F, cc->G = ctx->G, cc->C = C, cc->T = ctx->T, cc->Npad = ctx->Npad, cc->prec = precision;
+  cc->N = N, cc->F = F, cc->G = ctx->G, cc->C = C, cc->T = ctx->T, cc->Npad = ctx->Npad, cc->prec = ctx->prec;
   cc->U = U;
   hipStream_t st = ctx->stream;
   auto build = [&]() -> int {
@@ -1263,7 +1344,9 @@ int mmpfn_feature_attention(mmpfn_ctx* ctx, int layer, float* X, int S, int T, i
   RC(tap_check(ctx, layer, X, precision));
   if (S <= 0 || T <= 0) return fail(ctx, MMPFN_ERR_INVALID, "bad state geometry");
   RC(tap_workspace(ctx, S, T, 64));
-  return feat_sublayer(ctx, ctx->layers[layer], X, S, T, 1, base_prec(precision));
+  return state_tap(ctx, X, (int64_t)S * T * ctx->d.emsize, precision, T <= 64, [&](void* Xs, int bp) {
+    return feat_sublayer(ctx, ctx->layers[layer], Xs, S, T, 1, bp);
+  });
 }
 
 int mmpfn_item_attention_block(mmpfn_ctx* ctx, int layer, float* X, int S, int T, int N, int precision) {
@@ -1271,13 +1354,17 @@ int mmpfn_item_attention_block(mmpfn_ctx* ctx, int layer, float* X, int S, int T
   if (S <= 0 || T <= 0 || N <= 0 || N > S) return fail(ctx, MMPFN_ERR_INVALID, "bad state geometry");
   const int Npad = (N + 63) / 64 * 64;
   RC(tap_workspace(ctx, S, T, Npad));
-  return item_sublayer(ctx, layer, X, S, T, N, Npad, 1, base_prec(precision), false, f8_of(precision));
+  return state_tap(ctx, X, (int64_t)S * T * ctx->d.emsize, precision, true, [&](void* Xs, int bp) {
+    return item_sublayer(ctx, layer, Xs, S, T, N, Npad, 1, bp, false, f8_of(precision));
+  });
 }
 
 int mmpfn_mlp_ln(mmpfn_ctx* ctx, int layer, float* X, int64_t rows, int precision) {
   RC(tap_check(ctx, layer, X, precision));
   if (rows <= 0) return fail(ctx, MMPFN_ERR_INVALID, "bad row count");
-  return mlp_sublayer(ctx, ctx->layers[layer], X, rows, base_prec(precision), nullptr);
+  return state_tap(ctx, X, rows * ctx->d.emsize, precision, true, [&](void* Xs, int bp) {
+    return mlp_sublayer(ctx, ctx->layers[layer], Xs, rows, bp, nullptr);
+  });
 }
 
 int mmpfn_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int precision) {
@@ -1287,7 +1374,8 @@ int mmpfn_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* token
     return fail(ctx, MMPFN_ERR_INVALID, "model has no MGM head bank");
   if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
-  return mixer_mgm(ctx, image, S, n_mod, tokens, base_prec(precision));
+  const int bp = base_prec(precision);
+  return mixer_mgm(ctx, image, S, n_mod, tokens, bp == PREC_F16 ? PREC_BF16 : bp);
 }
 
 int mmpfn_cap(mmpfn_ctx* ctx, const float* mgm_tokens, int S, int M, float* tokens, int precision) {
@@ -1296,7 +1384,8 @@ int mmpfn_cap(mmpfn_ctx* ctx, const float* mgm_tokens, int S, int M, float* toke
   if (ctx->d.mixer_type != MMPFN_MIXER_MGM_CAP) return fail(ctx, MMPFN_ERR_INVALID, "model has no CAP");
   if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
-  return mixer_cap(ctx, mgm_tokens, S, M, tokens, base_prec(precision));
+  const int bp = base_prec(precision);
+  return mixer_cap(ctx, mgm_tokens, S, M, tokens, bp == PREC_F16 ? PREC_BF16 : bp);
 }
 
 }  // extern "C"

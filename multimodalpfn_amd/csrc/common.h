@@ -40,6 +40,35 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+typedef _Float16 f16;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+
+// 16-bit MFMA operand types of the performance modes: bf16 (PREC_BF16: fp32 state) or fp16 (PREC_F16:
+// fp16 state, the reference's autocast dtype); gfx950 runs both forms at one rate
+template <bool F16> struct Op16;
+template <> struct Op16<false> {
+  typedef __bf16 t;
+  typedef bf16x8 x8;
+  typedef bf16x4 x4;
+};
+template <> struct Op16<true> {
+  typedef _Float16 t;
+  typedef f16x8 x8;
+  typedef f16x4 x4;
+};
+__device__ __forceinline__ f32x4 mfma16x(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16x(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32x(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32x(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
 
 constexpr float kLog2e = 1.4426950408889634f;
 

@@ -493,4 +493,59 @@ hipError_t launch_decoder(const float* X, int Q, const float* w1t, const float* 
   return hipGetLastError();
 }
 
+// ---- PREC_F16 state conversions (the encoders and the decoder work in fp32; the layers keep an fp16 state)
+namespace {
+// out[b][r][:] = in[b][r][:] over nb blocks of rows x E elements with block strides (4 elements per thread)
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void cvt_rows_kernel(const TI* __restrict__ in, int64_t in_bstride, TO* __restrict__ out,
+                                                       int64_t out_bstride, int64_t per_block4, int nb) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= per_block4 * nb) return;
+  const int64_t b = i / per_block4, j = (i - b * per_block4) * 4;
+  const TI* s = in + b * in_bstride + j;
+  TO* d = out + b * out_bstride + j;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = (TO)(float)s[k];
+}
+// out[s][t][e] (fp32, reference order) = X[t][s][e] (fp16 state)
+__global__ __launch_bounds__(256) void state_f16_to_f32_kernel(const f16* __restrict__ X, float* __restrict__ out, int S,
+                                                               int T, int E) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n = (int64_t)S * T * E;
+  if (i >= n) return;
+  const int e = (int)(i % E);
+  const int64_t st = i / E;
+  const int t = (int)(st % T), s = (int)(st / T);
+  out[i] = (float)X[((int64_t)t * S + s) * E + e];
+}
+}  // namespace
+
+hipError_t launch_f32_to_f16(const float* in, int64_t in_bstride, void* out, int64_t out_bstride, int64_t per_block,
+                             int nb, hipStream_t st) {
+  if (per_block <= 0 || nb <= 0) return hipSuccess;
+  if (per_block % 4) return hipErrorInvalidValue;
+  const int64_t n4 = per_block / 4 * nb;
+  hipLaunchKernelGGL((cvt_rows_kernel<float, f16>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, in,
+                     in_bstride, (f16*)out, out_bstride, per_block / 4, nb);
+  return hipGetLastError();
+}
+
+hipError_t launch_f16_to_f32(const void* in, int64_t in_bstride, float* out, int64_t out_bstride, int64_t per_block,
+                             int nb, hipStream_t st) {
+  if (per_block <= 0 || nb <= 0) return hipSuccess;
+  if (per_block % 4) return hipErrorInvalidValue;
+  const int64_t n4 = per_block / 4 * nb;
+  hipLaunchKernelGGL((cvt_rows_kernel<f16, float>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st,
+                     (const f16*)in, in_bstride, out, out_bstride, per_block / 4, nb);
+  return hipGetLastError();
+}
+
+hipError_t launch_state_f16_to_f32(const void* X, float* out, int S, int T, int E, hipStream_t st) {
+  const int64_t n = (int64_t)S * T * E;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(state_f16_to_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const f16*)X, out, S,
+                     T, E);
+  return hipGetLastError();
+}
+
 }  // namespace mmpfn

@@ -24,6 +24,14 @@
 // the next head's in flight during the current head; the 78 KB out-projection image over both
 // buffers at the end.  80 KB of LDS and <= 256 VGPRs per 4-row block: two blocks per CU.
 // Per row: 6*(18*NT + NT^2 + 2*NT*ceil(NT/2)) + 72*NT MFMAs; HBM traffic = X read + written once.
+//
+// F16 (PREC_F16: the state X is fp16, the reference's autocast dtype): the row's X^T fragments are
+// loaded as they are stored (16-B loads, no conversion) and are the exact residual, so X is read once;
+// the out-projection image's rows are permuted (capi.cpp: pack_feat_rows res_perm) so that Y^T tile f
+// row 4g+i is feature 32(f>>1) + 8g + 4(f&1) + i -- the features of the lane's X fragments -- and
+// the normalised row is stored as 16-B pieces of 8 features.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -37,24 +45,26 @@ constexpr int FR_ST = FEAT_IMG_STRIDE;           // bf16 row stride of every LDS
 constexpr int FR_QKV_IMG = 96 * FR_ST;           // one head's QKV image: 19968 bf16 = 39 KB
 constexpr int FR_PIECES = FR_QKV_IMG * 2 / 1024; // 1-KB DMA pieces per QKV image (39)
 
-__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ bf16x8 cat8(const f32x4& a, const f32x4& b, float s = 1.0f) {
-  bf16x8 r;
+template <typename X8>
+__device__ __forceinline__ X8 cat8(const f32x4& a, const f32x4& b, float s = 1.0f) {
+  typedef decltype(X8{}[0]) T;
+  X8 r;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] = (bf16)(a[i] * s), r[4 + i] = (bf16)(b[i] * s);
+  for (int i = 0; i < 4; ++i) r[i] = (T)(a[i] * s), r[4 + i] = (T)(b[i] * s);
   return r;
 }
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-template <int NT>
-__global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* __restrict__ Xall,
-                                                                         const bf16* __restrict__ pack, int S, int T,
+template <int NT, bool F16>
+__global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* __restrict__ Xv,
+                                                                         const void* __restrict__ packv, int S, int T,
                                                                          int M, float eps) {
-  __shared__ __attribute__((aligned(1024))) bf16 wbuf[2 * FR_QKV_IMG];
+  typedef typename Op16<F16>::x8 X8;
+  typedef std::conditional_t<F16, f16, float> XT;  // state element
+  typedef typename Op16<F16>::t WT;
+  const WT* __restrict__ pack = (const WT*)packv;
+  __shared__ __attribute__((aligned(1024))) WT wbuf[2 * FR_QKV_IMG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
   const int row = blockIdx.x * 4 + wave;  // row over the batch: member row / S, table row row % S
@@ -62,40 +72,49 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* 
   const int rc = rowok ? row : M * S - 1;
   const int mem = rc / S, sr = rc - mem * S;
   const int64_t SE = (int64_t)S * FR_E;
-  float* __restrict__ X = Xall + (int64_t)mem * T * SE;
+  XT* __restrict__ X = (XT*)Xv + (int64_t)mem * T * SE;
 
   // LDS-DMA of `pieces` KB from src (global) to dst (LDS), KB piece p by wave p % 4
-  auto dma = [&](const bf16* src, bf16* dst, int pieces) {
+  // (non-dependent pointer types: a builtin call on a template-dependent type is checked at instantiation,
+  // where the host pass cannot resolve it, and the kernel's host stub is then silently dropped)
+  auto dma = [&](const void* srcv, void* dstv, int pieces) {
+    const uint16_t* src = (const uint16_t*)srcv;
+    uint16_t* dst = (uint16_t*)dstv;
     for (int p = wave; p < pieces; p += 4)
       __builtin_amdgcn_global_load_lds(src + p * 512 + lane * 8, (lds_void*)(dst + p * 512), 16, 0, 0);
   };
 
   dma(pack, wbuf, FR_PIECES);  // head 0 -> buffer 0
   // ---- the row's tokens as bf16 fragments (padding tokens t >= T are zero)
-  bf16x8 xf[NT][FR_E / 32];
+  X8 xf[NT][FR_E / 32];
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) {
     const int t = 16 * tt + n;
     const bool pad = tt == NT - 1 && t >= T;  // only the last tile holds padding (T > 16 (NT - 1))
-    const float* xr = X + (int64_t)(pad ? 0 : t) * SE + (int64_t)sr * FR_E + 8 * g;
+    const XT* xr = X + (int64_t)(pad ? 0 : t) * SE + (int64_t)sr * FR_E + 8 * g;
 #pragma unroll
     for (int ks = 0; ks < FR_E / 32; ++ks) {
-      f32x4 lo = *(const f32x4*)(xr + 32 * ks), hi = *(const f32x4*)(xr + 32 * ks + 4);
-      if (pad) lo = hi = f32x4{0.f, 0.f, 0.f, 0.f};
-      xf[tt][ks] = cat8(lo, hi);
+      if constexpr (F16) {
+        xf[tt][ks] = *(const f16x8*)(xr + 32 * ks);
+        if (pad) xf[tt][ks] = f16x8{};
+      } else {
+        f32x4 lo = *(const f32x4*)(xr + 32 * ks), hi = *(const f32x4*)(xr + 32 * ks + 4);
+        if (pad) lo = hi = f32x4{0.f, 0.f, 0.f, 0.f};
+        xf[tt][ks] = cat8<X8>(lo, hi);
+      }
     }
   }
   __syncthreads();  // (its vmcnt(0) retires the DMA too)
 
-  bf16x8 of[FR_H][NT];  // O^T fragments of every head (K-step h of the out-projection)
+  X8 of[FR_H][NT];  // O^T fragments of every head (K-step h of the out-projection)
 #pragma unroll
   for (int h = 0; h < FR_H; ++h) {
     if (h + 1 < FR_H) dma(pack + (h + 1) * FR_QKV_IMG, wbuf + ((h + 1) & 1) * FR_QKV_IMG, FR_PIECES);
     else dma(pack + FR_H * FR_QKV_IMG, wbuf, FR_PIECES);  // out-projection image, first half (buffer 0 is free)
-    const bf16* wq = wbuf + (h & 1) * FR_QKV_IMG;  // [96][FR_ST]: Q (permuted) | K (permuted) | V
+    const WT* wq = wbuf + (h & 1) * FR_QKV_IMG;  // [96][FR_ST]: Q (permuted) | K (permuted) | V
 
     // ---- Q^T, K^T (C^T tiles) of the row, K = 192 in 6 steps (V after, to bound live registers)
-    bf16x8 qf[NT], kf[NT];
+    X8 qf[NT], kf[NT];
     {
       f32x4 qa[2][NT], ka[2][NT];
 #pragma unroll
@@ -104,27 +123,28 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* 
         for (int tt = 0; tt < NT; ++tt) qa[f][tt] = ka[f][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < FR_E / 32; ++ks) {
-        bf16x8 wqf[2], wkf[2];
+        X8 wqf[2], wkf[2];
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
-          wqf[f] = *(const bf16x8*)(wq + (16 * f + n) * FR_ST + 32 * ks + 8 * g);
-          wkf[f] = *(const bf16x8*)(wq + (32 + 16 * f + n) * FR_ST + 32 * ks + 8 * g);
+          wqf[f] = *(const X8*)(wq + (16 * f + n) * FR_ST + 32 * ks + 8 * g);
+          wkf[f] = *(const X8*)(wq + (32 + 16 * f + n) * FR_ST + 32 * ks + 8 * g);
         }
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
           for (int f = 0; f < 2; ++f) {
-            qa[f][tt] = mfma16(wqf[f], xf[tt][ks], qa[f][tt]);
-            ka[f][tt] = mfma16(wkf[f], xf[tt][ks], ka[f][tt]);
+            qa[f][tt] = mfma16x(wqf[f], xf[tt][ks], qa[f][tt]);
+            ka[f][tt] = mfma16x(wkf[f], xf[tt][ks], ka[f][tt]);
           }
       }
 #pragma unroll
-      for (int tt = 0; tt < NT; ++tt) qf[tt] = cat8(qa[0][tt], qa[1][tt]), kf[tt] = cat8(ka[0][tt], ka[1][tt]);
+      for (int tt = 0; tt < NT; ++tt)
+        qf[tt] = cat8<X8>(qa[0][tt], qa[1][tt]), kf[tt] = cat8<X8>(ka[0][tt], ka[1][tt]);
     }
     __builtin_amdgcn_sched_barrier(0);  // phases in order: bounds the live registers (2 waves / SIMD)
     // ---- V (C tiles: lane = head dim, 4 consecutive tokens) -> V^T A fragments per key-tile pair
     constexpr int NKP = (NT + 1) / 2;  // key-tile pairs (K = 32 keys per P.V MFMA)
-    bf16x8 vfr[2][NKP];
+    X8 vfr[2][NKP];
     {
       f32x4 va[2][NT];
 #pragma unroll
@@ -133,19 +153,19 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* 
         for (int tt = 0; tt < NT; ++tt) va[f][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < FR_E / 32; ++ks) {
-        bf16x8 wvf[2];
+        X8 wvf[2];
 #pragma unroll
-        for (int f = 0; f < 2; ++f) wvf[f] = *(const bf16x8*)(wq + (64 + 16 * f + n) * FR_ST + 32 * ks + 8 * g);
+        for (int f = 0; f < 2; ++f) wvf[f] = *(const X8*)(wq + (64 + 16 * f + n) * FR_ST + 32 * ks + 8 * g);
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
-          for (int f = 0; f < 2; ++f) va[f][tt] = mfma16(xf[tt][ks], wvf[f], va[f][tt]);
+          for (int f = 0; f < 2; ++f) va[f][tt] = mfma16x(xf[tt][ks], wvf[f], va[f][tt]);
       }
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int kp = 0; kp < NKP; ++kp)
-          vfr[mt][kp] = cat8(va[mt][2 * kp], 2 * kp + 1 < NT ? va[mt][2 * kp + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
+          vfr[mt][kp] = cat8<X8>(va[mt][2 * kp], 2 * kp + 1 < NT ? va[mt][2 * kp + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
     }
     __builtin_amdgcn_sched_barrier(0);
 
@@ -154,7 +174,7 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* 
     for (int qt = 0; qt < NT; ++qt) {
       f32x4 st[NT];
 #pragma unroll
-      for (int kt = 0; kt < NT; ++kt) st[kt] = mfma16(kf[kt], qf[qt], f32x4{0.f, 0.f, 0.f, 0.f});
+      for (int kt = 0; kt < NT; ++kt) st[kt] = mfma16x(kf[kt], qf[qt], f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
       for (int i = 0; i < 4; ++i)  // only the last key tile holds padding keys (T > 16*(NT-1))
         if (16 * (NT - 1) + 4 * g + i >= T) st[NT - 1][i] = -INFINITY;
@@ -177,11 +197,11 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* 
       f32x4 oa[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int kp = 0; kp < NKP; ++kp) {
-        const bf16x8 pb = cat8(st[2 * kp], 2 * kp + 1 < NT ? st[2 * kp + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
+        const X8 pb = cat8<X8>(st[2 * kp], 2 * kp + 1 < NT ? st[2 * kp + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) oa[mt] = mfma16(vfr[mt][kp], pb, oa[mt]);
+        for (int mt = 0; mt < 2; ++mt) oa[mt] = mfma16x(vfr[mt][kp], pb, oa[mt]);
       }
-      of[h][qt] = cat8(oa[0], oa[1], inv);
+      of[h][qt] = cat8<X8>(oa[0], oa[1], inv);
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();  // DMA of the next image landed; this head's buffer is free
@@ -200,20 +220,30 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* 
       y[f] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int h = 0; h < FR_H; ++h)
-        y[f] = mfma16(*(const bf16x8*)(wbuf + (16 * f + n) * FR_ST + 32 * h + 8 * g), of[h][tt], y[f]);
+        y[f] = mfma16x(*(const X8*)(wbuf + (16 * f + n) * FR_ST + 32 * h + 8 * g), of[h][tt], y[f]);
     }
     const int t = 16 * tt + n;
     const bool pad = tt == NT - 1 && t >= T;
     const bool valid = rowok && !pad;
-    float* xr = X + (int64_t)(pad ? 0 : t) * SE + (int64_t)sr * FR_E + 4 * g;
+    XT* xr = X + (int64_t)(pad ? 0 : t) * SE + (int64_t)sr * FR_E + (F16 ? 8 : 4) * g;
     float sm = 0.f;
+    if constexpr (F16) {  // the residual is the lane's own X fragments (image rows permuted to match)
 #pragma unroll
-    for (int f = 0; f < FR_E / 16; ++f) {
-      const f32x4 xv = *(const f32x4*)(xr + 16 * f);
+      for (int f = 0; f < FR_E / 16; ++f)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        y[f][i] += xv[i];
-        sm += y[f][i];
+        for (int i = 0; i < 4; ++i) {
+          y[f][i] += (float)xf[tt][f >> 1][4 * (f & 1) + i];
+          sm += y[f][i];
+        }
+    } else {
+#pragma unroll
+      for (int f = 0; f < FR_E / 16; ++f) {
+        const f32x4 xv = *(const f32x4*)(xr + 16 * f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          y[f][i] += xv[i];
+          sm += y[f][i];
+        }
       }
     }
     const float mean = sum_rows4(sm) * (1.0f / FR_E);
@@ -227,30 +257,44 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(float* 
       }
     const float rs = 1.0f / sqrtf(sum_rows4(q) * (1.0f / FR_E) + eps);
     if (valid) {
+      if constexpr (F16) {  // features 32k + 8g .. +7 from tiles 2k, 2k+1: one 16-B store each
 #pragma unroll
-      for (int f = 0; f < FR_E / 16; ++f) {
-        f32x4 ov;
+        for (int k = 0; k < FR_E / 32; ++k) {
+          f16x8 ov;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ov[i] = (y[f][i] - mean) * rs;
-        *(f32x4*)(xr + 16 * f) = ov;
+          for (int i = 0; i < 4; ++i)
+            ov[i] = (f16)((y[2 * k][i] - mean) * rs), ov[4 + i] = (f16)((y[2 * k + 1][i] - mean) * rs);
+          *(f16x8*)(xr + 32 * k) = ov;
+        }
+      } else {
+#pragma unroll
+        for (int f = 0; f < FR_E / 16; ++f) {
+          f32x4 ov;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ov[i] = (y[f][i] - mean) * rs;
+          *(f32x4*)(xr + 16 * f) = ov;
+        }
       }
     }
   }
 }
 
+template <bool F16>
+hipError_t launch_fr(void* X, const void* pk, int S, int T, int M, float eps, hipStream_t st) {
+  const dim3 grid((M * S + 3) / 4), block(256);
+  if (T <= 16) hipLaunchKernelGGL((feat_rows_kernel<1, F16>), grid, block, 0, st, X, pk, S, T, M, eps);
+  else if (T <= 32) hipLaunchKernelGGL((feat_rows_kernel<2, F16>), grid, block, 0, st, X, pk, S, T, M, eps);
+  else if (T <= 48) hipLaunchKernelGGL((feat_rows_kernel<3, F16>), grid, block, 0, st, X, pk, S, T, M, eps);
+  else hipLaunchKernelGGL((feat_rows_kernel<4, F16>), grid, block, 0, st, X, pk, S, T, M, eps);
+  return hipGetLastError();
+}
 }  // namespace
 
-hipError_t launch_feat_rows(float* X, const void* pack, int S, int T, int M, int E, int H, float eps,
-                            hipStream_t st) {
+hipError_t launch_feat_rows(void* X, const void* pack, int S, int T, int M, int E, int H, float eps, hipStream_t st,
+                            bool f16) {
   if (S <= 0 || M <= 0) return hipSuccess;
   if (E != FR_E || H != FR_H || T < 1 || T > 64) return hipErrorInvalidValue;
-  const dim3 grid((M * S + 3) / 4), block(256);
-  const bf16* pk = (const bf16*)pack;
-  if (T <= 16) hipLaunchKernelGGL(feat_rows_kernel<1>, grid, block, 0, st, X, pk, S, T, M, eps);
-  else if (T <= 32) hipLaunchKernelGGL(feat_rows_kernel<2>, grid, block, 0, st, X, pk, S, T, M, eps);
-  else if (T <= 48) hipLaunchKernelGGL(feat_rows_kernel<3>, grid, block, 0, st, X, pk, S, T, M, eps);
-  else hipLaunchKernelGGL(feat_rows_kernel<4>, grid, block, 0, st, X, pk, S, T, M, eps);
-  return hipGetLastError();
+  return f16 ? launch_fr<true>(X, pack, S, T, M, eps, st) : launch_fr<false>(X, pack, S, T, M, eps, st);
 }
 
 }  // namespace mmpfn

@@ -11,13 +11,30 @@ namespace mmpfn {
 // bf16 hi + lo planes, x = hi + lo to 2^-17, and the three significant products hi.hi + hi.lo +
 // lo.hi accumulated in fp32 (the dropped lo.lo term is 2^-16 relative) -- 3 bf16 MFMAs at 16x the
 // fp32-input rate; PREC_F32_MFMA: the same forward on fp32-input MFMA (exact fp32 fma chains)
-// PREC_BF16_F8 / PREC_BF16_F8E5: PREC_BF16 with the sample-axis attention's P.V on block-scaled fp8
+// PREC_F16: the reference's fp16 autocast -- the inter-kernel state X stored in fp16, every layer
+// contraction on fp16 MFMA operands (the item attention's P.V on bf16: its P needs bf16's range), fp32
+// accumulation, LayerNorm and softmax statistics (featrow / rowgemm / mlp_rows / attention_pipe F16 forms)
+// PREC_*_F8 / PREC_*_F8E5: the 16-bit modes with the sample-axis attention's P.V on block-scaled fp8
 // MFMA (V^T e4m3; P e4m3 / e5m2; attention_pipe.hip) -- config E's fp8 path, opt-in
-enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1, PREC_F32_MFMA = 2, PREC_BF16_F8 = 3, PREC_BF16_F8E5 = 4 };
+enum Prec : int {
+  PREC_F32 = 0,
+  PREC_BF16 = 1,
+  PREC_F32_MFMA = 2,
+  PREC_BF16_F8 = 3,
+  PREC_BF16_F8E5 = 4,
+  PREC_F16 = 5,
+  PREC_F16_F8 = 6,
+  PREC_F16_F8E5 = 7
+};
 // the precision the layer kernels run in, and the fp8 P.V variant (0: none)
-inline int base_prec(int p) { return p == PREC_BF16_F8 || p == PREC_BF16_F8E5 ? PREC_BF16 : p; }
-inline int f8_of(int p) { return p == PREC_BF16_F8 ? 1 : p == PREC_BF16_F8E5 ? 2 : 0; }
-inline bool prec_ok(int p) { return p >= PREC_F32 && p <= PREC_BF16_F8E5; }
+inline int base_prec(int p) {
+  return p == PREC_BF16_F8 || p == PREC_BF16_F8E5 ? PREC_BF16 : p == PREC_F16_F8 || p == PREC_F16_F8E5 ? PREC_F16 : p;
+}
+inline int f8_of(int p) {
+  return p == PREC_BF16_F8 || p == PREC_F16_F8 ? 1 : p == PREC_BF16_F8E5 || p == PREC_F16_F8E5 ? 2 : 0;
+}
+inline bool prec_ok(int p) { return p >= PREC_F32 && p <= PREC_F16_F8E5; }
+inline bool prec16(int p) { return p == PREC_BF16 || p == PREC_F16; }  // a 16-bit performance mode (base)
 
 enum Epi : int {
   EPI_STORE = 0,      // C[row] = act(acc + bias)
@@ -76,26 +93,31 @@ hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M,
 // permuted hidden order of pack_mlp2_perm (capi.cpp); Fh % 32 == 0, E == 192
 // W1perm: W1 with its K (feature) order permuted to the Y^T lane layout (capi.cpp pack_mlp1_perm);
 // O / Wout non-null: X <- LN(X + O Wout^T) first (the item-attention out-projection, fused)
-hipError_t launch_mlp_rows(float* X, const void* W1perm, const void* W2perm, int64_t M, int E, int Fh, float eps,
-                           hipStream_t st, const void* O = nullptr, const void* Wout = nullptr);
+// f16 (PREC_F16): X / O fp16, W1 natural, W2 (pack_mlp2_perm) and Wout with f16_row_perm-ordered rows
+hipError_t launch_mlp_rows(void* X, const void* W1perm, const void* W2perm, int64_t M, int E, int Fh, float eps,
+                           hipStream_t st, const void* O = nullptr, const void* Wout = nullptr, bool f16 = false);
 
 // row-resident item-attention projections (bf16, K = 192, rowgemm.hip):
 //   QKV: X rows (remap (m/rdiv)*rmul + (m%rdiv)*rmul2 + roff) . W^T, W [N][192] (N = 576 or 192),
 //        scattered to Q [b][h][pos][32], K [b][h][pos][32] (Npad rows), V^T [b][h][32][Npad],
 //        b = m / rdiv, pos = roff + m % rdiv
 //   RES_LN: X <- LN(X + O . W^T), O [M][192] bf16, W [192][192] bf16
-hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
+//   f16 (PREC_F16): X fp16, W fp16, Q / K fp16 (V^T stays bf16); RES_LN: O / X fp16, W rows in
+//   f16_row_perm order (weight_pack.h)
+hipError_t launch_rowgemm_qkv(const void* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
                               const void* W, int M, int N, void* q, void* k, void* vt, int S, int Npad, int H,
-                              hipStream_t st);
+                              hipStream_t st, bool f16 = false);
 // two row sets (train rows: q|k|v, test rows: q) of the same token columns in ONE launch,
 // rows m -> memory row (m / rdiv) * a_rmul + m % rdiv + roff of each set
-hipError_t launch_rowgemm_qkv_pair(const float* X, int64_t rdiv1, int64_t roff1, const void* W1, int M1, int N1,
+hipError_t launch_rowgemm_qkv_pair(const void* X, int64_t rdiv1, int64_t roff1, const void* W1, int M1, int N1,
                                    int64_t rdiv2, int64_t roff2, const void* W2, int M2, int N2, int64_t a_rmul,
-                                   void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st);
+                                   void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st,
+                                   bool f16 = false);
 // C = (ln ? LayerNorm(A) : A) . W^T + bias: A fp32 [M][192], W [N][192] bf16, C bf16 [M][N], N % 64 == 0
 hipError_t launch_rowgemm_ln_store(const float* A, const void* W, const float* bias, void* C, int64_t M, int N,
                                    float eps, bool ln, hipStream_t st);
-hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, float* X, float eps, hipStream_t st);
+hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, void* X, float eps, hipStream_t st,
+                                bool f16 = false);
 
 // parity-mode (x3 split-bf16) row-resident projections of width 192 (rowgemm3.hip), fp32 in and out:
 // W = the hi plane [N][192] of capi.cpp upsplit, its lo plane at W + w_lo elements.
@@ -119,7 +141,9 @@ hipError_t launch_proj3_resln(const float* O, const void* W, int64_t w_lo, int64
 // permuted | Wv), then the out-projection [192][FEAT_IMG_STRIDE] with permuted head columns
 // (FEAT_IMG_STRIDE, FEAT_PACK_LAYER: weight_pack.h)
 // X holds M members [M][T][S][E]; one launch covers the M*S rows
-hipError_t launch_feat_rows(float* X, const void* pack, int S, int T, int M, int E, int H, float eps, hipStream_t st);
+// f16: PREC_F16 -- X fp16, pack the fp16 images with the out-projection rows permuted (pack_feat_rows res_perm)
+hipError_t launch_feat_rows(void* X, const void* pack, int S, int T, int M, int E, int H, float eps, hipStream_t st,
+                            bool f16 = false);
 
 // fused attention-between-features sublayer (bf16 only): X <- LN(X + MHA_feat(X)) per row,
 // wqkv [3*H*32][E] bf16, wout [E][H*32] bf16; rows per block = feat_block_rows(T) (0: unsupported T)
@@ -158,6 +182,7 @@ struct Attn2Args {
   int q_prescaled;     // Q already carries log2(e)/sqrt(32) (folded into the engine's bf16 Q weights)
   const unsigned char* vt8;  // f8 != 0: V^T in e4m3, the layout of vt
   int f8;              // P.V on fp8 MFMA: 0 off (bf16), 1 P in e4m3, 2 P in e5m2 (attention_pipe.hip)
+  int qk_f16;          // PREC_F16: q, k and o hold fp16 (S on f16 MFMA); vt stays bf16
 };
 // software-pipelined bf16 sample-axis attention (attention_pipe.hip); tasks of ATTN_ITEM_QPB queries
 constexpr int ATTN_ITEM_QPB = 256;
@@ -172,7 +197,7 @@ hipError_t launch_attn_pipe(const Attn2Args& a, hipStream_t st);
 hipError_t launch_attn_layer(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0,
                              bool q_prescaled = false,  // Q already scaled by log2(e)/sqrt(32)
-                             const void* vt8 = nullptr, int f8 = 0);
+                             const void* vt8 = nullptr, int f8 = 0, bool qk_f16 = false);
 // bf16 -> e4m3 (saturating) of n elements (n % 8 == 0): the F8 attention's V^T operand
 hipError_t launch_vt_fp8(const void* vt, void* vt8, int64_t n, hipStream_t st);
 // parity mode (PREC_F32) of launch_attn_layer on fp32 Q / K / V^T (split bf16 three-product MFMAs), fp32 O
@@ -206,6 +231,14 @@ hipError_t launch_add_tokens(const float* tok /*[S][C][E]*/, int S, int C, const
 hipError_t launch_decoder(const float* X /*[Q][E]*/, int Q, const float* w1t /*[E][Fh]*/, const float* b1, int Fh,
                           const float* w2, const float* b2, int n_out, float* out, int E, hipStream_t st, int M,
                           int64_t xm, int64_t om, float* scratch);
+
+// PREC_F16 state conversions: nb blocks of per_block elements (per_block % 4 == 0) at the given block
+// strides (elements); the state [T][S][E] fp16 -> the reference order [S][T][E] fp32
+hipError_t launch_f32_to_f16(const float* in, int64_t in_bstride, void* out, int64_t out_bstride, int64_t per_block,
+                             int nb, hipStream_t st);
+hipError_t launch_f16_to_f32(const void* in, int64_t in_bstride, float* out, int64_t out_bstride, int64_t per_block,
+                             int nb, hipStream_t st);
+hipError_t launch_state_f16_to_f32(const void* X, float* out, int S, int T, int E, hipStream_t st);
 
 hipError_t launch_aggregate(const float* logits /*[M][Q][n_out]*/, int M, int Q, int n_out,
                             const int* perms /*[M][n_cls] or null*/, int n_cls, float temp, int avg_before,

@@ -19,6 +19,13 @@
 // two blocks per CU) two chunks ahead of use, unpadded and XOR-swizzled (see the ring comment below).
 // Measured against register staging into two padded slots (in-step launch, rocprofv3): 168-171 ->
 // 162-163 us per two-member launch; a DMA ring whose peeled tail chunks spilled 130 VGPRs ran 197 us.
+//
+// F16 (PREC_F16): X and O are fp16 and every operand is fp16.  The output rows (W2, and Wout of the fused
+// prologue) are stored in f16_row_perm order (weight_pack.h), so Y^T tile f row 4g+i is feature
+// 32(f>>1) + 8g + 4(f&1) + i: a lane's 48 features are six 16-B runs of the fp16 row (one load / store
+// each), and the X^T fragments built from Y^T are in natural feature order (W1 unpermuted).
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -53,18 +60,30 @@ __device__ __forceinline__ void static_for(F&& f) {  // f(integral_constant<int,
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
 
 // TT = 16-row tiles per wave: 2 (32 rows, two waves per SIMD, accumulators in VGPRs) or 4 (64 rows,
 // one wave per SIMD with the 192 x 64 Y^T accumulator in AGPRs -- half the LDS weight reads per row,
 // but measured 15% slower: one wave cannot hide the LDS / GELU latency the second wave covers)
 // NW = waves per block: 4 (two blocks per CU, each DMA-filling its own rings) or 8 (one block per CU:
 // each weight byte crosses into LDS once per CU; waves 0-3 fill the W1 ring, 4-7 the W2 ring)
-template <int TT, bool RES, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_rows_kernel(float* __restrict__ X,
-                                                                       const bf16* __restrict__ W1,
-                                                                       const bf16* __restrict__ W2p, int M, int Fh,
-                                                                       float eps, const bf16* __restrict__ O,
-                                                                       const bf16* __restrict__ Wout) {
+template <int TT, bool RES, int NW, bool F16>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_rows_kernel(void* __restrict__ Xv,
+                                                                       const void* __restrict__ W1v,
+                                                                       const void* __restrict__ W2v, int M, int Fh,
+                                                                       float eps, const void* __restrict__ Ov,
+                                                                       const void* __restrict__ Woutv) {
+  typedef typename Op16<F16>::t HT;  // operand element
+  typedef typename Op16<F16>::x8 X8;
+  typedef __attribute__((ext_vector_type(2))) HT HT2;
+  float* __restrict__ X = (float*)Xv;  // bf16 mode: the fp32 state
+  f16* __restrict__ Xh = (f16*)Xv;     // F16: the fp16 state
+  const HT* __restrict__ W1 = (const HT*)W1v;
+  const HT* __restrict__ W2p = (const HT*)W2v;
+  const HT* __restrict__ O = (const HT*)Ov;
+  const HT* __restrict__ Wout = (const HT*)Woutv;
   constexpr int RROWS = NW * 16 * TT;  // rows per block
   __shared__ __attribute__((aligned(1024))) bf16 lds[LDS_B / 2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -97,14 +116,14 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
   }
   auto dma_w1 = [&](int c, int slot) {  // W1 rows c*32 .. +31
     if (!gw1) return;
-    const bf16* base = W1 + (int64_t)c * RHC * RE;
+    const HT* base = W1 + (int64_t)c * RHC * RE;
 #pragma unroll
     for (int j = 0; j < MP; ++j)
       mlp_dma16(o1[j], base, __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT_B + (wg * MP + j) * 1024));
   };
   auto dma_w2 = [&](int c, int slot) {  // W2 columns c*32 .. +31 (permuted), all 192 rows
     if (!gw2) return;
-    const bf16* base = W2p + c * RHC;
+    const HT* base = W2p + c * RHC;
 #pragma unroll
     for (int j = 0; j < MP; ++j)
       mlp_dma16(o2[j], base,
@@ -121,24 +140,34 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
 
   // ---- the wave's rows as B fragments in the Y^T lane layout: lane (row 16tt + fr, group fg)
   //      holds features 16f + 4fg + i; K position 32ks + 8fg + j <-> feature of tile f = 2ks + j/4
-  bf16x8 af[TT][RE / 32];
+  X8 af[TT][RE / 32];
   f32x4 y[RE / 16][TT];
   auto to_af = [&](int tt) {
 #pragma unroll
     for (int ks = 0; ks < RE / 32; ++ks) {
-      bf16x8 b;
+      X8 b;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) b[i] = (bf16)y[2 * ks][tt][i], b[4 + i] = (bf16)y[2 * ks + 1][tt][i];
+      for (int i = 0; i < 4; ++i) b[i] = (HT)y[2 * ks][tt][i], b[4 + i] = (HT)y[2 * ks + 1][tt][i];
       af[tt][ks] = b;
     }
   };
-  auto load_x = [&]() {  // y <- the fp32 residual rows X, in the Y^T accumulator layout
+  auto load_x = [&]() {  // y <- the residual rows X, in the Y^T accumulator layout
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
       const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
-      const float* xr = X + m * RE + fg * 4;
+      if constexpr (F16) {  // features 32k + 8fg .. +7 = tiles 2k, 2k+1 (f16_row_perm layout)
+        const f16* xr = Xh + m * RE + fg * 8;
 #pragma unroll
-      for (int f = 0; f < RE / 16; ++f) y[f][tt] = *(const f32x4*)(xr + f * 16);
+        for (int k = 0; k < RE / 32; ++k) {
+          const f16x8 h = *(const f16x8*)(xr + 32 * k);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) y[2 * k][tt][i] = (float)h[i], y[2 * k + 1][tt][i] = (float)h[4 + i];
+        }
+      } else {
+        const float* xr = X + m * RE + fg * 4;
+#pragma unroll
+        for (int f = 0; f < RE / 16; ++f) y[f][tt] = *(const f32x4*)(xr + f * 16);
+      }
     }
   };
   auto wait_vm = [](auto nc) {  // s_waitcnt vmcnt(N): all but this thread's N newest memory ops landed
@@ -170,12 +199,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
             mlp_dma16(ow[j], Wout + hf * 96 * RE,
                       __builtin_amdgcn_readfirstlane(lds0 + hf * 3 * SLOT_B + (wg * 9 + j) * 1024));
         if (hf == 0) {
-          bf16x8 ao[TT][RE / 32];
+          X8 ao[TT][RE / 32];
 #pragma unroll
           for (int tt = 0; tt < TT; ++tt) {
             const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
 #pragma unroll
-            for (int ks = 0; ks < RE / 32; ++ks) ao[tt][ks] = *(const bf16x8*)(O + m * RE + ks * 32 + fg * 8);
+            for (int ks = 0; ks < RE / 32; ++ks) ao[tt][ks] = *(const X8*)(O + m * RE + ks * 32 + fg * 8);
           }
 #pragma unroll
           for (int tt = 0; tt < TT; ++tt)
@@ -190,8 +219,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
       for (int ks = 0; ks < RE / 32; ++ks)
 #pragma unroll
         for (int fl = 0; fl < 6; ++fl) {
-          const bf16x8 w = *(const bf16x8*)(ldsb + HF * 3 * SLOT_B + fl * 16 * 384 + (ks >> 1) * 128 +
-                                            ((ks & 1) ? f1o : f1e));
+          const X8 w = *(const X8*)(ldsb + HF * 3 * SLOT_B + fl * 16 * 384 + (ks >> 1) * 128 +
+                                    ((ks & 1) ? f1o : f1e));
 #pragma unroll
           for (int tt = 0; tt < TT; ++tt) y[6 * HF + fl][tt] = mfma16(w, af[tt][ks], y[6 * HF + fl][tt]);
         }
@@ -255,20 +284,20 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
 
   // GELU of one adjacent pair q (0 .. 4 TT - 1: tile tt, half ht, elements 2 (q & 1) + 0, 1) of a chunk's
   // H^T accumulators, packed into its bf16 B fragment for the down-projection
-  auto gelu_pair = [&](auto qc, const f32x4 (&hs)[2][TT], bf16x8 (&hb)[TT]) {
+  auto gelu_pair = [&](auto qc, const f32x4 (&hs)[2][TT], X8 (&hb)[TT]) {
     constexpr int q = decltype(qc)::value, tt = q >> 2, ht = (q >> 1) & 1, i = 2 * (q & 1);
-    const bf16x2 pr =
-        __builtin_convertvector((float2_t){gelu_tanh_fast(hs[ht][tt][i]), gelu_tanh_fast(hs[ht][tt][i + 1])}, bf16x2);
+    const HT2 pr =
+        __builtin_convertvector((float2_t){gelu_tanh_fast(hs[ht][tt][i]), gelu_tanh_fast(hs[ht][tt][i + 1])}, HT2);
     hb[tt][4 * ht + i] = pr[0];
     hb[tt][4 * ht + i + 1] = pr[1];
   };
   // H^T [32 hidden][16 TT rows] = W1c . A^T  (W1c in W1 slot SL); with G, the previous chunk's GELU
   // (hs -> hb) rides in the k-steps' MFMA shadows (pairs 0..4TT-1 spread over the RE/32 k-steps)
-  auto hmma = [&](auto slc, f32x4 (&h)[2][TT], auto gc, const f32x4 (&hs)[2][TT], bf16x8 (&hb)[TT]) {
+  auto hmma = [&](auto slc, f32x4 (&h)[2][TT], auto gc, const f32x4 (&hs)[2][TT], X8 (&hb)[TT]) {
     constexpr bool G = decltype(gc)::value;
     constexpr int SL = decltype(slc)::value;
     auto w1frag = [&](int ht, int ks) {
-      return *(const bf16x8*)(ldsb + SL * SLOT_B + ht * 16 * 384 + (ks >> 1) * 128 + ((ks & 1) ? f1o : f1e));
+      return *(const X8*)(ldsb + SL * SLOT_B + ht * 16 * 384 + (ks >> 1) * 128 + ((ks & 1) ? f1o : f1e));
     };
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -278,7 +307,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
 #define MLP_PU 2
 #endif
     constexpr int PU = MLP_PU;  // k-steps of W1 fragments in flight ahead of their MFMAs
-    bf16x8 wa[PU][2];
+    X8 wa[PU][2];
 #pragma unroll
     for (int i = 0; i < PU; ++i)
 #pragma unroll
@@ -306,7 +335,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
   // accumulate onto it, so the residual is never written out and read back
   f32x4 h[2][TT];
   {
-    bf16x8 unused[TT];
+    X8 unused[TT];
     hmma(S0{}, h, std::false_type{}, h, unused);
   }
   // before chunk 0: W1(1) and W2(0) landed (only W2(1) may fly); the barrier also keeps chunk 0 from
@@ -327,7 +356,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     // GELU of chunk c (VALU) inside the up-projection MFMAs of chunk c+1.  No branch on MORE: the last
     // chunk's up-projection reads a slot holding an older chunk (landed, unused result), which costs 1/24
     // of the up-projections and measured 0.7 % faster than the branch (159.9 -> 158.8 us)
-    bf16x8 hb[TT];
+    X8 hb[TT];
     {
       f32x4 hn[2][TT];
       hmma(std::integral_constant<int, (PAR + 1) % 3>{}, hn, std::true_type{}, h, hb);
@@ -342,8 +371,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
 #define MLP_PF 4
 #endif
       constexpr int PF = MLP_PF;
-      auto w2frag = [&](int o) { return *(const bf16x8*)(ldsb + PAR * SLOT_B + o * 16 * 64 + f2); };
-      bf16x8 wb[PF];
+      auto w2frag = [&](int o) { return *(const X8*)(ldsb + PAR * SLOT_B + o * 16 * 64 + f2); };
+      X8 wb[PF];
 #pragma unroll
       for (int i = 0; i < PF; ++i) wb[i] = w2frag(i);
 #pragma unroll
@@ -399,12 +428,24 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     q = sum_rows4(q);
     const float inv = 1.0f / sqrtf(q * (1.0f / RE) + eps);
     if (valid) {
+      if constexpr (F16) {
+        f16* hr = Xh + m * RE + fg * 8;
 #pragma unroll
-      for (int o = 0; o < RE / 16; ++o) {
-        f32x4 ov;
+        for (int k = 0; k < RE / 32; ++k) {
+          f16x8 ov;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ov[i] = (y[o][tt][i] - mean) * inv;
-        *(f32x4*)(xr + o * 16) = ov;
+          for (int i = 0; i < 4; ++i)
+            ov[i] = (f16)((y[2 * k][tt][i] - mean) * inv), ov[4 + i] = (f16)((y[2 * k + 1][tt][i] - mean) * inv);
+          *(f16x8*)(hr + 32 * k) = ov;
+        }
+      } else {
+#pragma unroll
+        for (int o = 0; o < RE / 16; ++o) {
+          f32x4 ov;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ov[i] = (y[o][tt][i] - mean) * inv;
+          *(f32x4*)(xr + o * 16) = ov;
+        }
       }
     }
   }
@@ -412,10 +453,24 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
 
 }  // namespace
 
-hipError_t launch_mlp_rows(float* X, const void* W1perm, const void* W2perm, int64_t M, int E, int Fh, float eps,
-                           hipStream_t st, const void* O, const void* Wout) {
+namespace {
+template <bool F16>
+hipError_t launch_mr(void* X, const void* W1, const void* W2, int64_t M, int Fh, float eps, hipStream_t st,
+                     const void* O, const void* Wout);
+}  // namespace
+
+hipError_t launch_mlp_rows(void* X, const void* W1perm, const void* W2perm, int64_t M, int E, int Fh, float eps,
+                           hipStream_t st, const void* O, const void* Wout, bool f16) {
   if (M <= 0) return hipSuccess;
   if (E != RE || Fh % RHC != 0) return hipErrorInvalidValue;
+  return f16 ? launch_mr<true>(X, W1perm, W2perm, M, Fh, eps, st, O, Wout)
+             : launch_mr<false>(X, W1perm, W2perm, M, Fh, eps, st, O, Wout);
+}
+
+namespace {
+template <bool F16>
+hipError_t launch_mr(void* X, const void* W1perm, const void* W2perm, int64_t M, int Fh, float eps, hipStream_t st,
+                     const void* O, const void* Wout) {
 #ifndef MLP_TT
 #define MLP_TT 2  // 4 measured slower: 202 vs 175 us per two-member launch
 #endif
@@ -425,12 +480,13 @@ hipError_t launch_mlp_rows(float* X, const void* W1perm, const void* W2perm, int
   constexpr int RROWS = 16 * MLP_NW * MLP_TT;
   const dim3 grid((unsigned)((M + RROWS - 1) / RROWS)), block(64 * MLP_NW);
   if (O)
-    hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, true, MLP_NW>), grid, block, 0, st, X, (const bf16*)W1perm,
-                       (const bf16*)W2perm, (int)M, Fh, eps, (const bf16*)O, (const bf16*)Wout);
+    hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, true, MLP_NW, F16>), grid, block, 0, st, X, W1perm, W2perm, (int)M,
+                       Fh, eps, O, Wout);
   else
-    hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, false, MLP_NW>), grid, block, 0, st, X, (const bf16*)W1perm,
-                       (const bf16*)W2perm, (int)M, Fh, eps, nullptr, nullptr);
+    hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, false, MLP_NW, F16>), grid, block, 0, st, X, W1perm, W2perm, (int)M,
+                       Fh, eps, nullptr, nullptr);
   return hipGetLastError();
 }
+}  // namespace
 
 }  // namespace mmpfn

@@ -10,6 +10,13 @@
 // store); the V panel is computed untransposed (lane = head dim, 4 consecutive rows
 // -> one 8-byte store into V^T).  The RES_LN panel keeps Y^T in registers and does the
 // residual + LayerNorm across lanes (in-register permlane reductions).
+//
+// F16 (PREC_F16): X is the fp16 state -- a wave's fragments are 16-B loads of it, no conversion --,
+// the weights are fp16, Q / K are written in fp16 and V^T in bf16 (the attention's P.V runs on bf16:
+// its P = exp2(s) under a fixed reference needs bf16's exponent range); RES_LN reads O (fp16) and the
+// fp16 residual and uses f16_row_perm-ordered weight rows, so each lane's features are 16-B runs.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -25,22 +32,26 @@ constexpr int WPC = GE * GE / 8 / 256;  // 16-B panel pieces per thread (18)
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
 
 struct RgArgs {
-  const void* A;     // fp32 rows (QKV) or bf16 rows (RES_LN), ld = 192
+  const void* A;     // fp32 / fp16 (F16) rows (QKV) or 16-bit rows (RES_LN), ld = 192
   int64_t a_rdiv, a_rmul, a_rmul2, a_roff;  // logical row m -> memory row (m/rdiv)*rmul + (m%rdiv)*rmul2 + roff
-  const bf16* W;     // [N][192]
+  const void* W;     // [N][192] 16-bit
   int M, N;
-  // QKV scatter: b = m / a_rdiv, pos = a_roff + m % a_rdiv
-  bf16 *q, *k, *vt;
+  // QKV scatter: b = m / a_rdiv, pos = a_roff + m % a_rdiv (Q / K 16-bit of the mode, V^T bf16)
+  void *q, *k;
+  bf16* vt;
   int S, Npad, H;
   // RES_LN
-  float* X;
+  void* X;
   float eps;
 };
 
-template <bool AF32>
-__device__ __forceinline__ void load_rows(const RgArgs& p, int64_t m0, int fr, int fg, bf16x8 (&af)[2][GE / 32]) {
+template <bool AF32, typename X8>
+__device__ __forceinline__ void load_rows(const RgArgs& p, int64_t m0, int fr, int fg, X8 (&af)[2][GE / 32]) {
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const int m = (int)min(m0 + tt * 16 + fr, (int64_t)p.M - 1);
@@ -62,15 +73,15 @@ __device__ __forceinline__ void load_rows(const RgArgs& p, int64_t m0, int fr, i
         af[tt][ks] = b;
       }
     } else {
-      const bf16* xr = (const bf16*)p.A + mr * GE + fg * 8;
+      const uint16_t* xr = (const uint16_t*)p.A + mr * GE + fg * 8;
 #pragma unroll
-      for (int ks = 0; ks < GE / 32; ++ks) af[tt][ks] = *(const bf16x8*)(xr + ks * 32);
+      for (int ks = 0; ks < GE / 32; ++ks) af[tt][ks] = *(const X8*)(xr + ks * 32);
     }
   }
 }
 
 // stage W rows [n0, n0 + 192) into the LDS panel (all threads; caller brackets with barriers)
-__device__ __forceinline__ void stage_panel(const bf16* W, int n0, bf16* Ws, int tid) {
+__device__ __forceinline__ void stage_panel(const uint16_t* W, int n0, uint16_t* Ws, int tid) {
 #pragma unroll
   for (int half = 0; half < 2; ++half) {  // two rounds of 9 pieces: bounded register footprint
     u32x4 r[WPC / 2];
@@ -88,17 +99,17 @@ __device__ __forceinline__ void stage_panel(const bf16* W, int n0, bf16* Ws, int
 }
 
 // acc[f][tt] = panel(f) x rows(tt) over K = 192; TRANS: C^T (features x rows), else C (rows x features)
-template <bool TRANS>
-__device__ __forceinline__ void panel_mma(const bf16* Ws, const bf16x8 (&af)[2][GE / 32], int fr, int fg,
+template <bool TRANS, typename X8>
+__device__ __forceinline__ void panel_mma(const uint16_t* Ws, const X8 (&af)[2][GE / 32], int fr, int fg,
                                           f32x4 (&acc)[GE / 16][2]) {
 #pragma unroll
   for (int f = 0; f < GE / 16; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   // W fragments in groups of 4 feature tiles, the next group's reads issued before this
   // group's MFMAs (sched barriers keep the reads early; 2 x 4 fragments in flight)
   constexpr int NG = GE / 16 / 4;  // groups per k-step (3)
-  bf16x8 w[2][4];
+  X8 w[2][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) w[0][i] = *(const bf16x8*)(Ws + (i * 16 + fr) * WST + fg * 8);
+  for (int i = 0; i < 4; ++i) w[0][i] = *(const X8*)(Ws + (i * 16 + fr) * WST + fg * 8);
 #pragma unroll
   for (int it = 0; it < (GE / 32) * NG; ++it) {
     const int ks = it / NG, g = it % NG;
@@ -106,7 +117,7 @@ __device__ __forceinline__ void panel_mma(const bf16* Ws, const bf16x8 (&af)[2][
       const int ks1 = (it + 1) / NG, g1 = (it + 1) % NG;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        w[(it + 1) & 1][i] = *(const bf16x8*)(Ws + ((g1 * 4 + i) * 16 + fr) * WST + ks1 * 32 + fg * 8);
+        w[(it + 1) & 1][i] = *(const X8*)(Ws + ((g1 * 4 + i) * 16 + fr) * WST + ks1 * 32 + fg * 8);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -130,18 +141,18 @@ constexpr int QCP = QC * GE / 8 / 256;     // 16-B pieces per thread and chunk (
 
 // acc[f][tt] over K = 192 for one 64-feature chunk in LDS: the next k-step's 4 fragments are
 // read before this k-step's 8 MFMAs (sched barrier keeps them early)
-template <bool TRANS>
-__device__ __forceinline__ void chunk_mma(const bf16* W, const bf16x8 (&af)[2][GE / 32], int fr, int fg,
+template <bool TRANS, typename X8>
+__device__ __forceinline__ void chunk_mma(const uint16_t* W, const X8 (&af)[2][GE / 32], int fr, int fg,
                                           f32x4 (&acc)[QC / 16][2]) {
-  bf16x8 w[2][QC / 16];
+  X8 w[2][QC / 16];
 #pragma unroll
-  for (int f = 0; f < QC / 16; ++f) w[0][f] = *(const bf16x8*)(W + (f * 16 + fr) * WST + fg * 8);
+  for (int f = 0; f < QC / 16; ++f) w[0][f] = *(const X8*)(W + (f * 16 + fr) * WST + fg * 8);
 #pragma unroll
   for (int ks = 0; ks < GE / 32; ++ks) {
     if (ks + 1 < GE / 32)
 #pragma unroll
       for (int f = 0; f < QC / 16; ++f)
-        w[(ks + 1) & 1][f] = *(const bf16x8*)(W + (f * 16 + fr) * WST + (ks + 1) * 32 + fg * 8);
+        w[(ks + 1) & 1][f] = *(const X8*)(W + (f * 16 + fr) * WST + (ks + 1) * 32 + fg * 8);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int f = 0; f < QC / 16; ++f)
@@ -165,20 +176,25 @@ constexpr int OVST = 32 + 8;    // V^T tile row stride (bf16): 80 B
 constexpr int OWEL = QC * OVST; // per-wave staging elements (>= 32 * OQST)
 static_assert(32 * OQST <= OWEL, "Q/K staging tile must fit");
 
-__device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int bid, bf16* Ws) {
+template <bool F16>
+__device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int bid, uint16_t* Ws) {
+  typedef typename Op16<F16>::t OT;  // Q / K element
+  typedef typename Op16<F16>::x8 X8;
+  typedef typename Op16<F16>::x4 X4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int rd = (int)p.a_rdiv;
   const int b = bid / tiles_per_b;
   const int l0 = (bid - b * tiles_per_b) * GROWS + wave * 32;  // wave's first row inside column b
-  bf16* const Os = Ws + 2 * QCEL + wave * OWEL;
+  uint16_t* const Os = Ws + 2 * QCEL + wave * OWEL;
   const int nch = p.N / QC;
+  const uint16_t* Wg = (const uint16_t*)p.W;
   u32x4 r[QCP];
   auto fetch = [&](int c) {
 #pragma unroll
     for (int j = 0; j < QCP; ++j) {
       const int i = tid + 256 * j;
-      r[j] = *(const u32x4*)(p.W + (int64_t)(c * QC + i / (GE / 8)) * GE + (i % (GE / 8)) * 8);
+      r[j] = *(const u32x4*)(Wg + (int64_t)(c * QC + i / (GE / 8)) * GE + (i % (GE / 8)) * 8);
     }
   };
   auto stash = [&](int slot) {
@@ -189,8 +205,16 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
     }
   };
   fetch(0);
-  bf16x8 af[2][GE / 32];
-  {
+  X8 af[2][GE / 32];
+  if constexpr (F16) {  // the fp16 state is the operand: 16-B loads straight into the fragments
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int l = min(l0 + tt * 16 + fr, rd - 1);
+      const f16* xr = (const f16*)p.A + ((int64_t)b * p.a_rmul + (int64_t)l * p.a_rmul2 + p.a_roff) * GE + fg * 8;
+#pragma unroll
+      for (int ks = 0; ks < GE / 32; ++ks) af[tt][ks] = *(const f16x8*)(xr + ks * 32);
+    }
+  } else {
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
       const int l = min(l0 + tt * 16 + fr, rd - 1);
@@ -217,7 +241,7 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
   for (int c = 0; c < nch; ++c) {
     if (c + 1 < nch) stash((c + 1) & 1);
     if (c + 2 < nch) fetch(c + 2);
-    const bf16* W = Ws + (c & 1) * QCEL;
+    const uint16_t* W = Ws + (c & 1) * QCEL;
     const int n0 = c * QC, j = n0 / GE;  // 0 q, 1 k, 2 v
     const int h0 = (n0 - j * GE) >> 5;   // first of the chunk's two heads
     f32x4 acc[QC / 16][2];
@@ -230,13 +254,13 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int f = 0; f < QC / 16; ++f) {
-          bf16x4 o;
-          o[0] = (bf16)acc[f][tt][0], o[1] = (bf16)acc[f][tt][1];
-          o[2] = (bf16)acc[f][tt][2], o[3] = (bf16)acc[f][tt][3];
-          *(bf16x4*)(Os + (tt * 16 + fr) * OQST + f * 16 + fg * 4) = o;
+          X4 o;
+          o[0] = (OT)acc[f][tt][0], o[1] = (OT)acc[f][tt][1];
+          o[2] = (OT)acc[f][tt][2], o[3] = (OT)acc[f][tt][3];
+          *(X4*)(Os + (tt * 16 + fr) * OQST + f * 16 + fg * 4) = o;
         }
-      bf16* base = j == 0 ? p.q + (((int64_t)b * p.H + h0) * p.S + pos0) * 32
-                          : p.k + (((int64_t)b * p.H + h0) * p.Npad + pos0) * 32;
+      uint16_t* base = j == 0 ? (uint16_t*)p.q + (((int64_t)b * p.H + h0) * p.S + pos0) * 32
+                              : (uint16_t*)p.k + (((int64_t)b * p.H + h0) * p.Npad + pos0) * 32;
       const int64_t hstride = (int64_t)(j == 0 ? p.S : p.Npad) * 32;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
@@ -258,16 +282,17 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
           o[2] = (bf16)acc[f][tt][2], o[3] = (bf16)acc[f][tt][3];
           *(bf16x4*)(Os + (f * 16 + fr) * OVST + tt * 16 + fg * 4) = o;
         }
-      bf16* base = p.vt + ((int64_t)b * p.H + h0) * 32 * p.Npad + pos0;
+      uint16_t* base = (uint16_t*)p.vt + ((int64_t)b * p.H + h0) * 32 * p.Npad + pos0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int feat = 16 * i + (lane >> 2), rr = (lane & 3) * 8;
         const u32x4 v = *(const u32x4*)(Os + feat * OVST + rr);
-        bf16* dst = base + (int64_t)feat * p.Npad + rr;  // feature = (head - h0) * 32 + d
+        uint16_t* dst = base + (int64_t)feat * p.Npad + rr;  // feature = (head - h0) * 32 + d
         if (l0 + rr + 8 <= rd) {
           *(u32x4*)dst = v;
         } else {
-          const bf16x8 e = __builtin_bit_cast(bf16x8, v);
+          typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+          const u16x8 e = __builtin_bit_cast(u16x8, v);
 #pragma unroll
           for (int k = 0; k < 8; ++k)
             if (l0 + rr + k < rd) dst[k] = e[k];
@@ -281,11 +306,12 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
 // Two row sets in one launch: blocks [0, nblk1) project p's rows (the train rows: q|k|v), the
 // rest p2's (the test rows: q only, a third of the chunks) -- the short test-row blocks run last
 // and fill the grid's tail instead of a separate under-filled launch.
+template <bool F16>
 __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p, int tiles_per_b, const RgArgs p2,
                                                               int tiles2, int nblk1) {
-  __shared__ __attribute__((aligned(16))) bf16 Ws[2 * QCEL + 4 * OWEL];
-  if ((int)blockIdx.x < nblk1) qkv2_tile(p, tiles_per_b, blockIdx.x, Ws);
-  else qkv2_tile(p2, tiles2, blockIdx.x - nblk1, Ws);
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[2 * QCEL + 4 * OWEL];
+  if ((int)blockIdx.x < nblk1) qkv2_tile<F16>(p, tiles_per_b, blockIdx.x, Ws);
+  else qkv2_tile<F16>(p2, tiles2, blockIdx.x - nblk1, Ws);
 }
 
 // C[m] = (LN? LayerNorm(A[m]) : A[m]) . W^T + bias, A fp32 [M][192], W [N][192] bf16, C bf16 [M][N]
@@ -296,11 +322,11 @@ __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p, in
 __global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const float* __restrict__ A, const bf16* __restrict__ W,
                                                                   const float* __restrict__ bias, bf16* __restrict__ C,
                                                                   int M, int N, float eps, int do_ln) {
-  __shared__ __attribute__((aligned(16))) bf16 Ws[2 * QCEL + 4 * OWEL];
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[2 * QCEL + 4 * OWEL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * GROWS + wave * 32;
-  bf16* const Os = Ws + 2 * QCEL + wave * OWEL;
+  uint16_t* const Os = Ws + 2 * QCEL + wave * OWEL;
   const int nch = N / QC;
   u32x4 r[QCP];
   auto fetch = [&](int c) {
@@ -361,7 +387,7 @@ __global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const float* _
   for (int c = 0; c < nch; ++c) {
     if (c + 1 < nch) stash((c + 1) & 1);
     if (c + 2 < nch) fetch(c + 2);
-    const bf16* Wc = Ws + (c & 1) * QCEL;
+    const uint16_t* Wc = Ws + (c & 1) * QCEL;
     f32x4 acc[QC / 16][2];
 #pragma unroll
     for (int f = 0; f < QC / 16; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -382,33 +408,44 @@ __global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const float* _
     for (int i = 0; i < 4; ++i) {  // 32 rows x 8 chunks of 16 B
       const int row = 8 * i + (lane >> 3), cc = lane & 7;
       const u32x4 v = *(const u32x4*)(Os + row * OQST + cc * 8);
-      if (m0 + row < M) *(u32x4*)(C + (m0 + row) * N + c * QC + cc * 8) = v;
+      if (m0 + row < M) *(u32x4*)(C + (m0 + row) * N + c * QC + cc * 8) = v;  // (C: bf16 elements)
     }
     __syncthreads();
   }
 }
 
+template <bool F16>
 __global__ __launch_bounds__(256, 2) void rowgemm_resln_kernel(const RgArgs p) {
-  __shared__ __attribute__((aligned(16))) bf16 Ws[GE * WST];
+  typedef typename Op16<F16>::x8 X8;
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[GE * WST];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * GROWS + wave * 32;
-  stage_panel(p.W, 0, Ws, tid);
-  bf16x8 af[2][GE / 32];
+  stage_panel((const uint16_t*)p.W, 0, Ws, tid);
+  X8 af[2][GE / 32];
   load_rows<false>(p, m0, fr, fg, af);
   __syncthreads();
   f32x4 y[GE / 16][2];
   panel_mma<true>(Ws, af, fr, fg, y);
-  // Y^T: lane = row, rows of tile f = features 16f + 4fg + i
+  // Y^T: lane = row, rows of tile f = features 16f + 4fg + i (F16: f16_row_perm-ordered W rows, features
+  // 32(f>>1) + 8fg + 4(f&1) + i -- 16-B runs of the fp16 row)
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const int64_t m = m0 + tt * 16 + fr;
     const bool valid = m < p.M;
-    float* xr = p.X + (valid ? m : (int64_t)p.M - 1) * GE + fg * 4;
+    float* xr = (float*)p.X + (valid ? m : (int64_t)p.M - 1) * GE + fg * 4;
+    f16* hr = (f16*)p.X + (valid ? m : (int64_t)p.M - 1) * GE + fg * 8;
     float s = 0.f;
 #pragma unroll
     for (int f = 0; f < GE / 16; ++f) {
-      const f32x4 xv = *(const f32x4*)(xr + f * 16);
+      f32x4 xv;
+      if constexpr (F16) {
+        const f16x8 h8 = *(const f16x8*)(hr + (f >> 1) * 32);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xv[i] = (float)h8[4 * (f & 1) + i];
+      } else {
+        xv = *(const f32x4*)(xr + f * 16);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         y[f][tt][i] += xv[i];
@@ -428,12 +465,23 @@ __global__ __launch_bounds__(256, 2) void rowgemm_resln_kernel(const RgArgs p) {
     q = sum_rows4(q);
     const float inv = 1.0f / sqrtf(q * (1.0f / GE) + p.eps);
     if (valid) {
+      if constexpr (F16) {
 #pragma unroll
-      for (int f = 0; f < GE / 16; ++f) {
-        f32x4 ov;
+        for (int k = 0; k < GE / 32; ++k) {
+          f16x8 ov;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ov[i] = (y[f][tt][i] - mean) * inv;
-        *(f32x4*)(xr + f * 16) = ov;
+          for (int i = 0; i < 4; ++i)
+            ov[i] = (f16)((y[2 * k][tt][i] - mean) * inv), ov[4 + i] = (f16)((y[2 * k + 1][tt][i] - mean) * inv);
+          *(f16x8*)(hr + 32 * k) = ov;
+        }
+      } else {
+#pragma unroll
+        for (int f = 0; f < GE / 16; ++f) {
+          f32x4 ov;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ov[i] = (y[f][tt][i] - mean) * inv;
+          *(f32x4*)(xr + f * 16) = ov;
+        }
       }
     }
   }
@@ -443,7 +491,7 @@ __global__ __launch_bounds__(256, 2) void rowgemm_resln_kernel(const RgArgs p) {
 
 namespace {
 // one row set of the QKV projection: args, row tiles per column and block count (0 blocks: M == 0)
-hipError_t qkv_rowset(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff, const void* W,
+hipError_t qkv_rowset(const void* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff, const void* W,
                       int M, int N, void* q, void* k, void* vt, int S, int Npad, int H, RgArgs& a, int& tiles,
                       int64_t& nblk) {
   a = RgArgs{};
@@ -451,8 +499,8 @@ hipError_t qkv_rowset(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_
   if (M <= 0) return hipSuccess;
   if ((N != GE && N != 3 * GE) || H * 32 != GE) return hipErrorInvalidValue;
   a.A = X, a.a_rdiv = a_rdiv, a.a_rmul = a_rmul, a.a_rmul2 = a_rmul2, a.a_roff = a_roff;
-  a.W = (const bf16*)W, a.M = M, a.N = N;
-  a.q = (bf16*)q, a.k = (bf16*)k, a.vt = (bf16*)vt, a.S = S, a.Npad = Npad, a.H = H;
+  a.W = W, a.M = M, a.N = N;
+  a.q = q, a.k = k, a.vt = (bf16*)vt, a.S = S, a.Npad = Npad, a.H = H;
   // blocks tile each column b separately: nb = M / a_rdiv columns of a_rdiv rows
   if (a_rdiv <= 0 || M % a_rdiv != 0) return hipErrorInvalidValue;
   if (N == 3 * GE && (a_roff % 8 != 0 || a_roff + a_rdiv > Npad)) return hipErrorInvalidValue;  // 16-B V^T stores
@@ -462,21 +510,24 @@ hipError_t qkv_rowset(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_
 }
 }  // namespace
 
-hipError_t launch_rowgemm_qkv(const float* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
+hipError_t launch_rowgemm_qkv(const void* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
                               const void* W, int M, int N, void* q, void* k, void* vt, int S, int Npad, int H,
-                              hipStream_t st) {
+                              hipStream_t st, bool f16) {
   RgArgs a;
   int tiles;
   int64_t nblk;
   hipError_t e = qkv_rowset(X, a_rdiv, a_rmul, a_rmul2, a_roff, W, M, N, q, k, vt, S, Npad, H, a, tiles, nblk);
   if (e != hipSuccess || nblk == 0) return e;
-  hipLaunchKernelGGL(rowgemm_qkv2_kernel, dim3((unsigned)nblk), dim3(256), 0, st, a, tiles, a, tiles, (int)nblk);
+  if (f16)
+    hipLaunchKernelGGL(rowgemm_qkv2_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, st, a, tiles, a, tiles, (int)nblk);
+  else
+    hipLaunchKernelGGL(rowgemm_qkv2_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, st, a, tiles, a, tiles, (int)nblk);
   return hipGetLastError();
 }
 
-hipError_t launch_rowgemm_qkv_pair(const float* X, int64_t rdiv1, int64_t roff1, const void* W1, int M1, int N1,
+hipError_t launch_rowgemm_qkv_pair(const void* X, int64_t rdiv1, int64_t roff1, const void* W1, int M1, int N1,
                                    int64_t rdiv2, int64_t roff2, const void* W2, int M2, int N2, int64_t a_rmul,
-                                   void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st) {
+                                   void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st, bool f16) {
   RgArgs a1, a2;
   int t1, t2;
   int64_t n1, n2;
@@ -486,16 +537,21 @@ hipError_t launch_rowgemm_qkv_pair(const float* X, int64_t rdiv1, int64_t roff1,
   if (e != hipSuccess) return e;
   if (n1 + n2 == 0) return hipSuccess;
   if (n1 == 0) a1 = a2, t1 = t2;  // blocks index the second set only
-  hipLaunchKernelGGL(rowgemm_qkv2_kernel, dim3((unsigned)(n1 + n2)), dim3(256), 0, st, a1, t1, a2, t2, (int)n1);
+  if (f16)
+    hipLaunchKernelGGL(rowgemm_qkv2_kernel<true>, dim3((unsigned)(n1 + n2)), dim3(256), 0, st, a1, t1, a2, t2, (int)n1);
+  else
+    hipLaunchKernelGGL(rowgemm_qkv2_kernel<false>, dim3((unsigned)(n1 + n2)), dim3(256), 0, st, a1, t1, a2, t2, (int)n1);
   return hipGetLastError();
 }
 
-hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, float* X, float eps, hipStream_t st) {
+hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, void* X, float eps, hipStream_t st, bool f16) {
   if (M <= 0) return hipSuccess;
   RgArgs a{};
   a.A = O, a.a_rdiv = 1, a.a_rmul = 1, a.a_rmul2 = 0, a.a_roff = 0;
-  a.W = (const bf16*)W, a.M = (int)M, a.N = GE, a.X = X, a.eps = eps;
-  hipLaunchKernelGGL(rowgemm_resln_kernel, dim3((unsigned)((M + GROWS - 1) / GROWS)), dim3(256), 0, st, a);
+  a.W = W, a.M = (int)M, a.N = GE, a.X = X, a.eps = eps;
+  const dim3 grid((unsigned)((M + GROWS - 1) / GROWS));
+  if (f16) hipLaunchKernelGGL(rowgemm_resln_kernel<true>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(rowgemm_resln_kernel<false>, grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

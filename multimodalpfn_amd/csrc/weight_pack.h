@@ -24,6 +24,28 @@ inline uint16_t f2bf(float f) {  // round-to-nearest-even, NaN preserving
   return (uint16_t)(u >> 16);
 }
 
+// IEEE binary16, round-to-nearest-even (overflow -> inf, NaN preserved, subnormals kept)
+inline uint16_t f2h(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  const uint32_t sign = (u >> 16) & 0x8000u, a = u & 0x7fffffffu;
+  if (a > 0x7f800000u) return (uint16_t)(sign | 0x7e00u | ((a >> 13) & 0x3ffu));  // NaN
+  if (a >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // rounds to >= 65520: inf
+  if (a < 0x38800000u) {  // below the smallest normal half (2^-14): subnormal or zero
+    if (a < 0x33000000u) return (uint16_t)sign;  // < 2^-25: rounds to 0
+    const uint32_t m = (a & 0x7fffffu) | 0x800000u;
+    const int shift = 126 - (int)(a >> 23);  // 14..24 -> value = m >> shift (in units of 2^-24)
+    uint32_t r = m >> shift;
+    const uint32_t rem = m & ((1u << shift) - 1), half = 1u << (shift - 1);
+    if (rem > half || (rem == half && (r & 1))) ++r;
+    return (uint16_t)(sign | r);
+  }
+  uint32_t r = ((a - 0x38000000u) >> 13);  // rebias 127 -> 15
+  const uint32_t rem = a & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (r & 1))) ++r;
+  return (uint16_t)(sign | r);
+}
+
 // w_out [H][d][E] -> W[e][h*d+dd]
 inline std::vector<float> transpose_out(const std::vector<float>& w, int HD, int E) {
   std::vector<float> o((size_t)E * HD);
@@ -43,6 +65,19 @@ inline std::vector<float> pack_mlp2_perm(const std::vector<float>& w, int E, int
         const int hid = j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4);
         o[(size_t)e * Fh + c + pos] = w[(size_t)e * Fh + c + hid];
       }
+  return o;
+}
+
+// PREC_F16 row layout of a 192-wide output accumulated as Y^T 16x16 tiles: tile f row 4g+i holds
+// feature 32(f>>1) + 8g + 4(f&1) + i, so a lane's 48 features are its 6 runs of 8 (16-B fp16 pieces)
+inline int f16_row_perm(int r) {
+  const int f = r >> 4, rho = r & 15;
+  return 32 * (f >> 1) + 8 * (rho >> 2) + 4 * (f & 1) + (rho & 3);
+}
+// rows of W [E][K] permuted by f16_row_perm (image row r <- W row f16_row_perm(r))
+inline std::vector<float> permute_rows_f16(const std::vector<float>& w, int E, int K) {
+  std::vector<float> o(w.size());
+  for (int r = 0; r < E; ++r) std::memcpy(&o[(size_t)r * K], &w[(size_t)f16_row_perm(r) * K], K * sizeof(float));
   return o;
 }
 
@@ -67,8 +102,10 @@ inline std::vector<float> pack_mlp1_perm(const std::vector<float>& w, int E, int
 //        perm(8g+j) = j<4 ? 4g+j : 16+4g+(j-4)
 // qkv: w_qkv [3][H][32][E] (multi_head_attention.py:423-430); wout_t: [E][H*32].  H = 6, E = 192
 // (the kernel's and FEAT_PACK_LAYER's shape; the caller checks).
+// res_perm (PREC_F16): the out-projection rows in f16_row_perm order, so the Y^T tiles hold the
+// features of the lane's X fragments (the residual is added from registers)
 inline std::vector<float> pack_feat_rows(const std::vector<float>& qkv, const std::vector<float>& wout_t, int H,
-                                         int E) {
+                                         int E, bool res_perm = false) {
   const float c = 1.4426950408889634f / std::sqrt(32.0f);
   const int ST = FEAT_IMG_STRIDE;
   std::vector<float> o((size_t)FEAT_PACK_LAYER, 0.0f);
@@ -83,13 +120,15 @@ inline std::vector<float> pack_feat_rows(const std::vector<float>& qkv, const st
     }
   }
   float* po = o.data() + (size_t)H * 96 * ST;
-  for (int e = 0; e < E; ++e)
+  for (int e = 0; e < E; ++e) {
+    const int src = res_perm ? f16_row_perm(e) : e;
     for (int h = 0; h < H; ++h)
       for (int cc = 0; cc < 32; ++cc) {
         const int g = cc >> 3, jj = cc & 7;
         const int dd = jj < 4 ? 4 * g + jj : 16 + 4 * g + (jj - 4);
-        po[(size_t)e * ST + 32 * h + cc] = wout_t[(size_t)e * H * 32 + h * 32 + dd];
+        po[(size_t)e * ST + 32 * h + cc] = wout_t[(size_t)src * H * 32 + h * 32 + dd];
       }
+  }
   return o;
 }
 

@@ -37,7 +37,7 @@ from multimodalpfn_amd.utils import infer_random_state
 def _precision(model, device: torch.device, autocast: bool, forced: torch.dtype | None) -> int:
     if forced is not None:
         return _lib.precision_of_dtype(forced)
-    return _lib.PREC_BF16 if (autocast and device.type == "cuda") else _lib.f32_precision()
+    return _lib.autocast_precision() if (autocast and device.type == "cuda") else _lib.f32_precision()
 
 
 def _h2d(a, device: torch.device) -> torch.Tensor:

@@ -342,7 +342,7 @@ class PerFeatureTransformer(nn.Module):
         if self._forced_dtype is not None:
             return _lib.precision_of_dtype(self._forced_dtype)
         if torch.is_autocast_enabled(device.type):
-            return _lib.PREC_BF16
+            return _lib.autocast_precision()
         return _lib.f32_precision()
 
     # ------------------------------------------------------------------ forward

@@ -46,13 +46,20 @@ int main(int argc, char** argv) {
   }
   ok &= dump(dir, "f2bf_in.bin", bits) && dump(dir, "f2bf_out.bin", fout);
 
+  {  // fp16 rounding (PREC_F16 weights): every class, subnormals, overflow
+    std::vector<uint16_t> hout(bits.size());
+    for (size_t i = 0; i < bits.size(); ++i) hout[i] = f2h(fin[i]);
+    ok &= dump(dir, "f2h_out.bin", hout);
+  }
   ok &= dump(dir, "transpose_out.bin", transpose_out(iota_f((size_t)E * E), E, E));
+  ok &= dump(dir, "rows_f16.bin", permute_rows_f16(iota_f((size_t)E * Fh), E, Fh));
   ok &= dump(dir, "mlp1.bin", pack_mlp1_perm(iota_f((size_t)Fh * E), E, Fh));
   ok &= dump(dir, "mlp2.bin", pack_mlp2_perm(iota_f((size_t)E * Fh), E, Fh));
   {
     std::vector<float> qkv = iota_f((size_t)3 * H * 32 * E), wout = iota_f((size_t)E * H * 32);
     for (float& x : wout) x = -x;  // out-projection values distinct from the QKV ones
     ok &= dump(dir, "feat_rows.bin", pack_feat_rows(qkv, wout, H, E));
+    ok &= dump(dir, "feat_rows_f16.bin", pack_feat_rows(qkv, wout, H, E, true));
   }
   {
     const int N = 576, K = E;

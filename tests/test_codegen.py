@@ -61,17 +61,21 @@ def _blocks(body: str) -> list[collections.Counter]:
     return out
 
 
-def test_attention_tile_bodies_have_no_register_shuffles():
-    """The pipelined loop (attention_pipe.hip) is one basic block of six tiles: per tile 64 v_exp_f32,
-    32 v_cvt_pk_bf16_f32, 16 + 8 MFMAs and a handful of address / loop ops, no register shuffles."""
-    body = _function(_asm("attention_pipe.hip", ["-fno-honor-nans"]), "attn_pipe_kernelILi0E")
+@pytest.mark.parametrize("qk,smfma", [("Lb0E", "v_mfma_f32_32x32x16_bf16"), ("Lb1E", "v_mfma_f32_32x32x16_f16")])
+def test_attention_tile_bodies_have_no_register_shuffles(qk, smfma):
+    """The pipelined loop (attention_pipe.hip) is one basic block of four tiles: per tile 64 v_exp_f32,
+    32 v_cvt_pk_bf16_f32, 16 + 8 MFMAs and a handful of address / loop ops, no register shuffles (bf16 Q / K,
+    and the fp16 Q / K of PREC_F16, whose 8 score MFMAs per tile are the f16 form)."""
+    body = _function(_asm("attention_pipe.hip", ["-fno-honor-nans"]), f"attn_pipe_kernelILi0E{qk}")
+    pvm = "v_mfma_f32_32x32x16_bf16"
     loops = [c for c in _blocks(body) if c["v_exp_f32_e32"] >= 256 and c["v_exp_f32_e32"] % 64 == 0
-             and c["v_mfma_f32_32x32x16_bf16"] * 4 == c["v_exp_f32_e32"] and c["v_cndmask_b32_e64"] == 0]
-    assert len(loops) == 1, [(c["v_exp_f32_e32"], c["v_mfma_f32_32x32x16_bf16"]) for c in _blocks(body)]
+             and (c[smfma] + c[pvm] * (smfma != pvm)) * 4 == c["v_exp_f32_e32"] and c["v_cndmask_b32_e64"] == 0]
+    assert len(loops) == 1, [(c["v_exp_f32_e32"], c[smfma], c[pvm]) for c in _blocks(body)]
     c = loops[0]
     tiles = c["v_exp_f32_e32"] // 64
     valu = sum(v for k, v in c.items() if k.startswith("v_") and not k.startswith("v_mfma"))
     movs = c["v_mov_b32_e32"] + c["v_mov_b64_e32"]
+    assert c[smfma] + c[pvm] * (smfma != pvm) == 16 * tiles and c[pvm] >= 8 * tiles
     assert c["v_mfma_f32_16x16x32_bf16"] == 8 * tiles and c["v_cvt_pk_bf16_f32"] == 32 * tiles
     assert movs <= tiles and valu <= 100 * tiles, (valu, movs)
 
@@ -81,7 +85,7 @@ def test_fp8_attention_tile_bodies(variant, cvt):
     """The fp8 P.V variants (config E): per tile 64 exps, 8 score MFMAs (bf16), one 32x32x64 P.V and one
     16x16x128 row-sum MFMA per chain (block-scaled f8f6f4), 32 scaled conversions, no register shuffles
     (a defined `old` word of the packed conversions once cost 16 v_mov per tile)."""
-    body = _function(_asm("attention_pipe.hip", ["-fno-honor-nans"]), f"attn_pipe_kernelILi{variant}E")
+    body = _function(_asm("attention_pipe.hip", ["-fno-honor-nans"]), f"attn_pipe_kernelILi{variant}ELb0E")
     loops = [c for c in _blocks(body) if c["v_exp_f32_e32"] >= 256 and c["v_exp_f32_e32"] % 64 == 0
              and c["v_mfma_f32_32x32x16_bf16"] * 8 == c["v_exp_f32_e32"]]
     assert len(loops) == 1, [(c["v_exp_f32_e32"], c["v_mfma_f32_32x32x16_bf16"]) for c in _blocks(body)]
@@ -99,7 +103,8 @@ def test_fp8_attention_tile_bodies(variant, cvt):
     ("mlp_rows.hip", "mlp_rows_kernelILi2ELb1E", 0),
     ("mlp_rows.hip", "mlp_rows_kernelILi2ELb0E", 0),
     ("rowgemm.hip", "rowgemm_qkv2_kernel", 0),
-    ("featrow.hip", "feat_rows_kernelILi3E", 48),  # one-time spills outside the head loop
+    ("featrow.hip", "feat_rows_kernelILi3ELb0E", 48),  # one-time spills outside the head loop
+    ("featrow.hip", "feat_rows_kernelILi3ELb1E", 56),  # PREC_F16: X^T fragments live to the residual
 ])
 def test_layer_kernels_spills(src, needle, limit):
     extra = ["-fno-honor-nans"] if src in ("attention.hip", "attention_pipe.hip", "featrow.hip") else []
@@ -109,16 +114,17 @@ def test_layer_kernels_spills(src, needle, limit):
     assert max(hits.values()) <= limit, hits
 
 
-def test_mlp_gelu_rides_in_the_up_projection():
+@pytest.mark.parametrize("variant,mm", [("Lb0E", "v_mfma_f32_16x16x32_bf16"), ("Lb1E", "v_mfma_f32_16x16x32_f16")])
+def test_mlp_gelu_rides_in_the_up_projection(variant, mm):
     """The previous chunk's GELU once sank past the `if (MORE) hmma` branch into the down-projection's
     block, whose MFMAs consume it.  Now each chunk is one block (up-projection of the next
     chunk + this chunk's GELU + down-projection, 48 MFMAs, 16 exps); only the pre-loop up-projection of
     chunk 0 (24 MFMAs) has no GELU to carry."""
-    body = _function(_asm("mlp_rows.hip"), "mlp_rows_kernelILi2ELb1E")
-    mm = [c for c in _blocks(body) if 24 <= c["v_mfma_f32_16x16x32_bf16"] < 72]
-    bare = [c for c in mm if c["v_exp_f32_e32"] == 0]
-    chunks = [c for c in mm if c["v_mfma_f32_16x16x32_bf16"] == 48 and c["v_exp_f32_e32"] == 16]
-    assert len(bare) <= 1 and len(chunks) >= 3, ([(c["v_mfma_f32_16x16x32_bf16"], c["v_exp_f32_e32"]) for c in mm])
+    body = _function(_asm("mlp_rows.hip"), f"mlp_rows_kernelILi2ELb1ELi4E{variant}")
+    blocks = [c for c in _blocks(body) if 24 <= c[mm] < 72]
+    bare = [c for c in blocks if c["v_exp_f32_e32"] == 0]
+    chunks = [c for c in blocks if c[mm] == 48 and c["v_exp_f32_e32"] == 16]
+    assert len(bare) <= 1 and len(chunks) >= 3, ([(c[mm], c["v_exp_f32_e32"]) for c in blocks])
 
 
 def test_mlp_eight_wave_option_does_not_spill():

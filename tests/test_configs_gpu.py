@@ -30,6 +30,7 @@ S_ROWS, N_TRAIN, N_FEAT, N_CAT, N_CLS = 2298, 1838, 21, 18, 6
 FULL = {"C": (64, 24, 1, 2), "C-mgm256": (256, 24, 1, 2), "D": (64, 24, 2, 3)}
 BF16_BAND = {"C": 3.5e-2, "C-mgm256": 3.5e-2, "D": 2e-2}  # measured 1.64e-2, 1.77e-2, 0.99e-2
 BF16_AGREE = {"C": 0.995, "C-mgm256": 0.995, "D": 0.995}  # measured 1.00 on all three
+F16_BAND = 2e-2  # fp16 mode (MMPFN_PREC_F16, the reference's autocast dtype), all three configs
 
 
 def _model(cfg, sd):
@@ -67,10 +68,14 @@ def test_full_size_config_matches_oracle(name):
     x = torch.from_numpy(synth_table(S_ROWS, N_FEAT, seed, n_cat=N_CAT)).cuda()
     im = torch.from_numpy(synth_image(S_ROWS, n_mod, seed)).cuda()
     y = torch.from_numpy(synth_labels(S_ROWS, N_CLS, seed)[:N_TRAIN]).cuda()
+    from multimodalpfn_amd import _lib
+
     with torch.inference_mode():
         f32 = model(None, x[:, None, :], im, y, single_eval_pos=N_TRAIN).squeeze(1).float().cpu().numpy()
-        with torch.autocast("cuda"):
-            b16 = model(None, x[:, None, :], im, y, single_eval_pos=N_TRAIN).squeeze(1).float().cpu().numpy()
+        b16 = model(None, x[:, None, :], im, y, single_eval_pos=N_TRAIN,
+                    precision=_lib.PREC_BF16).squeeze(1).float().cpu().numpy()
+        h16 = model(None, x[:, None, :], im, y, single_eval_pos=N_TRAIN,
+                    precision=_lib.PREC_F16).squeeze(1).float().cpu().numpy()
     model.invalidate_engine()
     w = {k: v.cuda() for k, v in torch_sd(sd).items()}
     ref = oracle_forward(oracle_spec(cfg), w, x, im, y).cpu().numpy()
@@ -78,15 +83,19 @@ def test_full_size_config_matches_oracle(name):
     torch.cuda.empty_cache()
     assert ref.shape == (S_ROWS - N_TRAIN, cfg.n_out)
     assert np.isfinite(f32).all() and np.isfinite(b16).all()
-    e32, eb = rel_err(f32, ref), rel_err(b16, ref)
+    e32, eb, eh = rel_err(f32, ref), rel_err(b16, ref), rel_err(h16, ref)
     agree = float((b16.argmax(1) == ref.argmax(1)).mean())
     _log({"config": name, "S": S_ROWS, "N": N_TRAIN, "mgm": mgm, "cap": cap, "n_mod": n_mod,
           "f32_rel_err": e32, "f32_argmax_equal": bool((f32.argmax(1) == ref.argmax(1)).all()),
-          "bf16_rel_err": eb, "bf16_argmax_agree": agree, "ref_absmax": float(np.abs(ref).max())})
+          "bf16_rel_err": eb, "bf16_argmax_agree": agree, "f16_rel_err": eh,
+          "f16_argmax_agree": float((h16.argmax(1) == ref.argmax(1)).mean()), "ref_absmax": float(np.abs(ref).max())})
     assert e32 <= F32_TOL, (name, e32)
     assert (f32.argmax(1) == ref.argmax(1)).all()
     assert eb <= BF16_BAND[name], (name, eb)
     check_argmax(b16, ref, BF16_AGREE[name], f"bf16 {name}")
+    assert np.isfinite(h16).all()
+    assert eh <= F16_BAND, (name, eh)
+    check_argmax(h16, ref, BF16_AGREE[name], f"f16 {name}")
 
 
 def _ragged_members(n, seed, tok_n):

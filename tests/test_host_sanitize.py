@@ -62,6 +62,33 @@ def test_f2bf_matches_torch(outputs):
     assert np.array_equal(mine[nan] >> 15, (bits[nan] >> 31).astype(np.uint16))
 
 
+def test_f2h_matches_torch(outputs):
+    bits = outputs("f2bf_in.bin", np.uint32)
+    mine = outputs("f2h_out.bin", np.uint16)
+    x = torch.from_numpy(bits.view(np.float32).copy())
+    ref = x.to(torch.float16).view(torch.int16).numpy().view(np.uint16)
+    nan = np.isnan(bits.view(np.float32))
+    assert np.array_equal(mine[~nan], ref[~nan])
+    assert np.all((mine[nan] & 0x7C00) == 0x7C00) and np.all((mine[nan] & 0x03FF) != 0)
+
+
+def _f16_row_perm(r):  # tile f row 4g+i <- feature 32(f>>1) + 8g + 4(f&1) + i
+    f, rho = r >> 4, r & 15
+    return 32 * (f >> 1) + 8 * (rho >> 2) + 4 * (f & 1) + (rho & 3)
+
+
+def test_f16_row_permutation(outputs):
+    perm = _f16_row_perm(np.arange(E))
+    assert sorted(perm.tolist()) == list(range(E))
+    w = np.arange(E * FH, dtype=np.float32).reshape(E, FH)
+    assert np.array_equal(outputs("rows_f16.bin", np.float32).reshape(E, FH), w[perm])
+    # a lane (g) of Y^T tiles 2k, 2k+1 holds the 8 consecutive features 32k + 8g .. +7 (one 16-B fp16 run)
+    for k in range(E // 32):
+        for g in range(4):
+            feats = [_f16_row_perm(16 * (2 * k + t) + 4 * g + i) for t in range(2) for i in range(4)]
+            assert feats == list(range(32 * k + 8 * g, 32 * k + 8 * g + 8))
+
+
 def test_transpose_out(outputs):
     o = outputs("transpose_out.bin", np.float32).reshape(E, E)
     assert np.array_equal(o, np.arange(E * E, dtype=np.float32).reshape(E, E).T)
@@ -102,6 +129,14 @@ def test_feat_rows_images(outputs):
     cc = np.arange(H * 32)
     ref[H * 96:, :H * 32] = wout[:, 32 * (cc // 32) + _perm32(cc % 32)]
     assert np.array_equal(o.reshape(-1, ST), ref)
+
+
+def test_feat_rows_images_f16(outputs):
+    """PREC_F16 images: the QKV part as in bf16; the out-projection rows in f16_row_perm order."""
+    o = outputs("feat_rows_f16.bin", np.float32).reshape(-1, ST)
+    b = outputs("feat_rows.bin", np.float32).reshape(-1, ST)
+    assert np.array_equal(o[:H * 96], b[:H * 96])
+    assert np.array_equal(o[H * 96:], b[H * 96:][_f16_row_perm(np.arange(E))])
 
 
 def test_fold_ln(outputs):

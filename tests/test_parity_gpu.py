@@ -20,6 +20,8 @@ F32_TOL = 1e-4
 LARGE_BF16_TOL = {"B": 2.5e-2, "E": 3.5e-2}  # measured 1.28e-2 and 1.80e-2 (profiles/r02)
 BF16_AGREE = 0.995  # argmax agreement; measured 1.00 on every golden and on B / E (profiles/r02)
 F8_TOL = 5e-2  # config E with the fp8 P.V (MMPFN_PREC_BF16_F8 / _F8E5) against the oracle
+F16_TOL = 1e-2  # fp16 mode (MMPFN_PREC_F16: fp16 state and operands, the reference's autocast dtype)
+LARGE_F16_TOL = {"B": 2e-2, "E": 2e-2}
 BF16_TOL = 2e-2  # measured 3.1e-3 .. 9.5e-3 over the goldens (profiles/r02/pytest_gpu_r02a.log)
 
 
@@ -34,12 +36,13 @@ def make_model(cfg, sd):
     return model.to("cuda")
 
 
-def run_case(z, model, autocast=False):
+def run_case(z, model, autocast=False, precision=None):
     x = torch.from_numpy(z["x"])[:, None, :].cuda() if "x" in z else None
     im = torch.from_numpy(z["image"]).cuda() if "image" in z else None
     y = torch.from_numpy(z["y_train"]).cuda()
+    kw = {} if precision is None else {"precision": precision}
     with torch.autocast("cuda", enabled=autocast), torch.inference_mode():
-        out = model(None, x, im, y, only_return_standard_out=True, categorical_inds=[], single_eval_pos=len(y))
+        out = model(None, x, im, y, only_return_standard_out=True, categorical_inds=[], single_eval_pos=len(y), **kw)
     return out.squeeze(1).float().cpu().numpy()
 
 
@@ -74,6 +77,22 @@ def test_forward_bf16_close_to_reference(case):
     print(f"bf16 {case}: rel err {err:.3e}")
     assert err <= BF16_TOL, err
     check_argmax(out, z["logits"], BF16_AGREE, f"bf16 {case}")
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_forward_f16_close_to_reference(case):
+    """MMPFN_PREC_F16 (the reference's fp16 autocast: fp16 state between kernels, fp16 MFMA operands)."""
+    from multimodalpfn_amd import _lib
+
+    z, meta, cfg, sd = load_case(case)
+    model = make_model(cfg, sd)
+    out = run_case(z, model, precision=_lib.PREC_F16)
+    b16 = run_case(z, model, precision=_lib.PREC_BF16)
+    assert np.isfinite(out).all()
+    err, eb = rel_err(out, z["logits"]), rel_err(b16, z["logits"])
+    print(f"f16 {case}: rel err {err:.3e} (bf16 {eb:.3e})")
+    assert err <= F16_TOL, err
+    check_argmax(out, z["logits"], BF16_AGREE, f"f16 {case}")
 
 
 def test_embedding_and_layer_taps_fp32():
@@ -385,8 +404,9 @@ def test_engine_deterministic_and_no_nan_at_pad_ufes_size():
     check_argmax(c.squeeze(1).numpy(), a.squeeze(1).numpy(), 0.995, "config C bf16 vs fp32 engine")
 
 
+@pytest.mark.parametrize("prec", [1, 5])
 @pytest.mark.parametrize("lanes,batch", [(2, 1), (3, 1), (1, 2), (1, 5), (2, 2), (2, 3)])
-def test_forward_lanes_match_sequential(lanes, batch):
+def test_forward_lanes_match_sequential(lanes, batch, prec):
     """Members batched into one forward ([M][T][S][E] state) and/or on concurrent lanes (own
     workspace + stream each) == one member after another, bitwise."""
     from synth import synth_image, synth_labels, synth_state_dict, synth_table
@@ -410,8 +430,8 @@ def test_forward_lanes_match_sequential(lanes, batch):
         ym = rng.permutation(3)[y.astype(np.int64)].astype(np.float32)
         items.append((xm, tok, ym))
     with torch.inference_mode():
-        seq = eng.forward_many(items, _lib.PREC_BF16, lanes=1, batch=1)
-        par = eng.forward_many(items, _lib.PREC_BF16, lanes=lanes, batch=batch)
+        seq = eng.forward_many(items, prec, lanes=1, batch=1)
+        par = eng.forward_many(items, prec, lanes=lanes, batch=batch)
         eng.status()
     for a, b in zip(seq, par):
         assert torch.equal(a.cpu(), b.cpu())
@@ -515,10 +535,12 @@ def test_large_config_matches_oracle_on_device(name, S, N, F, n_cls, seed):
     f8 = {}
     with torch.inference_mode():
         f32 = model(None, x[:, None, :], None, y, single_eval_pos=N).squeeze(1).float().cpu().numpy()
-        with torch.autocast("cuda"):
-            b16 = model(None, x[:, None, :], None, y, single_eval_pos=N).squeeze(1).float().cpu().numpy()
+        b16 = model(None, x[:, None, :], None, y, single_eval_pos=N,
+                    precision=_lib.PREC_BF16).squeeze(1).float().cpu().numpy()
+        h16 = model(None, x[:, None, :], None, y, single_eval_pos=N,
+                    precision=_lib.PREC_F16).squeeze(1).float().cpu().numpy()
         if name[0] == "E":  # config E's fp8 path: P.V + row sums on block-scaled fp8 MFMA
-            for fmt, code in (("e4m3", _lib.PREC_BF16_F8), ("e5m2", _lib.PREC_BF16_F8E5)):
+            for fmt, code in (("e4m3", _lib.PREC_BF16_F8), ("e5m2", _lib.PREC_BF16_F8E5), ("f16+e4m3", _lib.PREC_F16_F8)):
                 f8[fmt] = model(None, x[:, None, :], None, y, single_eval_pos=N,
                                 precision=code).squeeze(1).float().cpu().numpy()
     w = {k: v.cuda() for k, v in torch_sd(sd).items()}
@@ -532,6 +554,10 @@ def test_large_config_matches_oracle_on_device(name, S, N, F, n_cls, seed):
     print(f"bf16 {name}: rel err {eb:.3e}; fp32 rel err {rel_err(f32, ref):.3e}")
     assert eb <= LARGE_BF16_TOL[name[0]], (name, eb)
     check_argmax(b16, ref, BF16_AGREE, f"bf16 {name}")
+    eh = rel_err(h16, ref)
+    print(f"f16 {name}: rel err {eh:.3e}, argmax agreement {float((h16.argmax(1) == ref.argmax(1)).mean()):.4f}")
+    assert eh <= LARGE_F16_TOL[name[0]], (name, eh)
+    check_argmax(h16, ref, BF16_AGREE, f"f16 {name}")
     for fmt, out in f8.items():
         e8 = rel_err(out, ref)
         agree = float((out.argmax(1) == ref.argmax(1)).mean())
@@ -541,8 +567,8 @@ def test_large_config_matches_oracle_on_device(name, S, N, F, n_cls, seed):
         check_argmax(out, ref, BF16_AGREE, f"fp8 {fmt} {name}")
 
 
-@pytest.mark.parametrize("prec", [0, 1])
-def test_train_kv_cache_equals_full_forward(prec):
+@pytest.mark.parametrize("prec", [0, 1, 5])
+def test_train_kv_cache_equals_full_forward(prec):  # (0 parity, 1 bf16, 5 fp16)
     """mmpfn_cache_build (train rows once) + mmpfn_cache_predict (test rows only) == the test
     rows of one full forward, bitwise (every kernel computes a row independently of the others;
     the encoders' statistics come from the train rows in both)."""
