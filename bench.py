@@ -54,7 +54,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
+    p.add_argument("--precision", choices=["f16", "bf16", "f32"], default="f16",
+                   help="f16: MMPFN_PREC_F16, the reference's fp16 autocast (fp16 state + operands); bf16: bf16 "
+                        "operands on an fp32 state; f32: the parity mode")
     p.add_argument("--members", type=int, default=MEMBERS_PER_GPU, help="members per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--attn-reps", type=int, default=20)
@@ -146,27 +148,33 @@ def live_roofline(lib, ctx, T_launch):
     }
 
 
-def time_item_attention(eng, T, reps, S=S_ROWS, N=N_TRAIN):
+def time_item_attention(eng, T, reps, S=S_ROWS, N=N_TRAIN, precision=None):
     """Average launch duration of the sample-axis attention kernel at the workload's shape.
 
     One launch = the whole attention-between-items of one layer (train rows on their own
-    heads + test rows of all heads on head 0's K/V), HIP events on the engine stream."""
+    heads + test rows of all heads on head 0's K/V), HIP events on the engine stream.  ``precision``:
+    an engine code of mmpfn_item_attention_layer_ex (bf16 / f16 Q and K, optionally the fp8 P.V); the
+    fp8 codes include the V^T conversion launch in the time."""
+    from multimodalpfn_amd import _lib
+
     H, d = 6, 32
     Q = S - N
     Npad = (N + 63) // 64 * 64
     dev = eng.device
+    precision = _lib.PREC_BF16 if precision is None else precision
+    qk_dt = torch.float16 if precision in (_lib.PREC_F16, _lib.PREC_F16_F8, _lib.PREC_F16_F8E5) else torch.bfloat16
     g = torch.Generator(device="cpu").manual_seed(0)
-    q = torch.randn(T, H, S, d, generator=g).to(dev, torch.bfloat16)
-    k = torch.randn(T, H, Npad, d, generator=g).to(dev, torch.bfloat16)
+    q = torch.randn(T, H, S, d, generator=g).to(dev, qk_dt)
+    k = torch.randn(T, H, Npad, d, generator=g).to(dev, qk_dt)
     vt = torch.randn(T, H, d, Npad, generator=g).to(dev, torch.bfloat16)
-    o = torch.empty(T, S, H * d, device=dev, dtype=torch.bfloat16)
+    o = torch.empty(T, S, H * d, device=dev, dtype=qk_dt)
     lib, ctx = eng.lib, eng.ctx
     eng._bind_stream()
     stream = torch.cuda.current_stream(dev)
 
     def launch():
-        rc = lib.mmpfn_item_attention_layer(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), S, T, H,
-                                            Npad, N)
+        rc = lib.mmpfn_item_attention_layer_ex(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), S, T, H,
+                                               Npad, N, precision)
         assert rc == 0, lib.mmpfn_last_error(ctx)
 
     for _ in range(3):
@@ -381,7 +389,7 @@ def api_end_to_end(cfg, sd, x, y, image, n_estimators, prec_f32, steps, world, p
 def _lib_prec(f32: bool) -> int:
     from multimodalpfn_amd import _lib
 
-    return _lib.PREC_F32 if f32 else _lib.PREC_BF16
+    return _lib.PREC_F32 if f32 else _lib.autocast_precision()
 
 
 def timed_steps(step, steps, warmup, world, device):
@@ -543,7 +551,9 @@ def main():
     from multimodalpfn_amd import _lib
     from multimodalpfn_amd.parallel import lpt_assign, member_cost
 
-    prec = _lib.PREC_BF16 if args.precision == "bf16" else _lib.PREC_F32
+    prec = {"f16": _lib.PREC_F16, "bf16": _lib.PREC_BF16, "f32": _lib.PREC_F32}[args.precision]
+    # the classifier legs (api_end_to_end) run inference_precision="auto" = the reference's fp16 autocast
+    os.environ["MMPFN_AUTOCAST"] = "f16" if prec == _lib.PREC_F16 else "bf16"
     cfg, sd, model, x, y, image, members = build_workload(device, world, args.members)
     eng = model.engine(device)
     img = torch.from_numpy(image).to(device)
@@ -593,6 +603,19 @@ def main():
                 "one lane: launches run one after another, as in `bench.py --lanes 1`")
             live["in_step_overlapped"] = {k: live_ovl[k] for k in ("achieved", "frac", "per_launch_ms", "timing")}
 
+    # ---- the other 16-bit mode (bf16 operands on an fp32 state, or the fp16 mode), same step
+    other16 = None
+    if prec in (_lib.PREC_F16, _lib.PREC_BF16):
+        p2 = _lib.PREC_BF16 if prec == _lib.PREC_F16 else _lib.PREC_F16
+        step2 = make_step(eng, members, mine, assignment, rank, img, p2, args.lanes, args.batch)
+        k2 = max(3, args.steps // 3)
+        dt2 = timed_steps(step2, k2, 2, world, device)
+        other16 = {"value": round(M * S_ROWS * k2 / dt2, 1), "unit": "rows/s", "ms_per_step": round(dt2 / k2 * 1e3, 3),
+                   "steps": k2, "dtype": "bf16" if p2 == _lib.PREC_BF16 else "f16",
+                   "note": ("MMPFN_PREC_BF16: bf16 MFMA operands on an fp32 state" if p2 == _lib.PREC_BF16 else
+                            "MMPFN_PREC_F16: fp16 state between kernels and fp16 MFMA operands (the reference's "
+                            "fp16 autocast)") + ", the same step"}
+
     # ---- the fp32 parity mode (what the 1e-4 logits contract costs)
     f32 = None
     if args.f32_leg and prec != _lib.PREC_F32:
@@ -631,11 +654,22 @@ def main():
             roof["isolated_same_shape_launch"] = {k: isb[k] for k in ("achieved", "frac", "per_launch_ms", "traffic")}
         # the same kernel at BASELINE.json's other single-GPU shapes (one layer's launch, alone):
         # B = 4096 support x 100 features (G = 50, T = 51), E = 10k support rows (G = 10, T = 11)
+        # (the headline mode's Q / K precision; config E also with the fp8 P.V of MMPFN_PREC_*_F8 / _F8E5, whose
+        # times include the V^T -> e4m3 conversion launch)
         roof["other_configs_isolated_launch"] = {}
-        for name, (Tc, Sc, Nc) in {"B: S=5120 N=4096 T=51": (51, 5120, 4096),
-                                   "E: S=12000 N=10000 T=11": (11, 12000, 10000)}.items():
-            r = time_item_attention(eng, Tc, max(3, args.attn_reps // 4), Sc, Nc)
-            roof["other_configs_isolated_launch"][name] = {k: r[k] for k in ("achieved", "frac", "per_launch_ms")}
+        p16 = prec if prec in (_lib.PREC_F16, _lib.PREC_BF16) else _lib.PREC_BF16
+        f8s = ((_lib.PREC_F16_F8, _lib.PREC_F16_F8E5) if p16 == _lib.PREC_F16 else
+               (_lib.PREC_BF16_F8, _lib.PREC_BF16_F8E5))
+        shapes = {"B: S=5120 N=4096 T=51": (51, 5120, 4096, (p16,)),
+                  "E: S=12000 N=10000 T=11": (11, 12000, 10000, (p16,) + f8s)}
+        names = {_lib.PREC_F16: "", _lib.PREC_BF16: "", _lib.PREC_F16_F8: " fp8 P.V (P e4m3)",
+                 _lib.PREC_BF16_F8: " fp8 P.V (P e4m3)", _lib.PREC_F16_F8E5: " fp8 P.V (P e5m2)",
+                 _lib.PREC_BF16_F8E5: " fp8 P.V (P e5m2)"}
+        for name, (Tc, Sc, Nc, codes) in shapes.items():
+            for code in codes:
+                r = time_item_attention(eng, Tc, max(3, args.attn_reps // 4), Sc, Nc, code)
+                roof["other_configs_isolated_launch"][name + names[code]] = {
+                    k: r[k] for k in ("achieved", "frac", "per_launch_ms")}
     eng.close()
     cfg_d = config_d_leg(device, world, rank, args, prec) if args.config_d else None
     mod = None
@@ -661,7 +695,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if prec == _lib.PREC_BF16 else "f32",
+            "dtype": {_lib.PREC_F16: "f16", _lib.PREC_BF16: "bf16"}.get(prec, "f32"),
             "data": "synthetic (PAD-UFES-20 shape; random-init weights of the MMPFN architecture)",
             "config": {
                 "workload": "config C: PAD-UFES-20 image+tabular, N=1838 support + Q=460 query rows, F=21 "
@@ -695,6 +729,7 @@ def main():
             "cpu_baseline_einsum": cpu_e,
             "api_end_to_end": api,
             "api_end_to_end_default_preprocessing": api_def,
+            "other_16bit_mode": other16,
             "f32_parity_mode": f32,
             "config_D": cfg_d,
             "kv_cache_predict": kv,

@@ -174,10 +174,11 @@ int mmpfn_select_lane(mmpfn_ctx* ctx, int lane);
 int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
                                int T, int H, int Npad, int N);
 
-/* mmpfn_item_attention_layer with the fp8 P.V of MMPFN_PREC_BF16_F8 (p_format 1: P e4m3) or
- * MMPFN_PREC_BF16_F8E5 (p_format 2: P e5m2); vt is the bf16 V^T (converted to e4m3 inside). */
-int mmpfn_item_attention_layer_fp8(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
-                                   int T, int H, int Npad, int N, int p_format);
+/* mmpfn_item_attention_layer in a 16-bit precision code: MMPFN_PREC_BF16 (as mmpfn_item_attention_layer),
+ * MMPFN_PREC_F16 (q, k and out in fp16, vt bf16), or either with the fp8 P.V (MMPFN_PREC_*_F8: P e4m3,
+ * *_F8E5: P e5m2; vt is the bf16 V^T, converted to e4m3 inside). */
+int mmpfn_item_attention_layer_ex(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
+                                  int T, int H, int Npad, int N, int precision);
 
 /* The train-KV cache's attention (bf16 only): queries s in [0, S) of every head against a
  * head-0-only K [T][Npad][32] / V^T [T][32][Npad] (the layout mmpfn_cache_build keeps per

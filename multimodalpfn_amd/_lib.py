@@ -108,7 +108,7 @@ SIGNATURES = [
     ("mmpfn_item_attention", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i]),
     ("mmpfn_item_attention_layer", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i]),
     ("mmpfn_item_attention_cached", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i]),
-    ("mmpfn_item_attention_layer_fp8", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i]),
+    ("mmpfn_item_attention_layer_ex", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i]),
     ("mmpfn_select_lane", _i, [_vp, _i]),
     ("mmpfn_forward_batch", _i, [_vp, _i, _vp, _i, _i, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _i]),
     ("mmpfn_cache_build", _i, [_vp, _vp, _i, _i, _vp, _i, _vp, _vp, _i, _vp, _i, ctypes.POINTER(_vp)]),

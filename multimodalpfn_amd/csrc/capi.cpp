@@ -1306,17 +1306,21 @@ int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, con
   return MMPFN_OK;
 }
 
-int mmpfn_item_attention_layer_fp8(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
-                                   int T, int H, int Npad, int N, int p_format) {
+int mmpfn_item_attention_layer_ex(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
+                                  int T, int H, int Npad, int N, int precision) {
   if (!ctx || !q || !k || !vt || !out) return MMPFN_ERR_INVALID;
-  if (N <= 0 || N > S || N > Npad || Npad % 64 || H <= 0 || H > 8 || T <= 0 || (p_format != 1 && p_format != 2))
+  if (N <= 0 || N > S || N > Npad || Npad % 64 || H <= 0 || H > 8 || T <= 0)
     return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
+  if (!prec_ok(precision) || !prec16(base_prec(precision))) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
-  const int64_t n = (int64_t)T * H * 32 * Npad;
-  RC(ensure(ctx, ctx->tap_v8, (size_t)n));
-  HIPCHK(launch_vt_fp8(vt, ctx->tap_v8.p, n, ctx->stream));
-  HIPCHK(launch_attn_layer(q, k, vt, out, S, T, H, Npad, N, 0, N, N, S - N, 0, ctx->stream, 0, false, ctx->tap_v8.p,
-                           p_format));
+  const int f8 = f8_of(precision);
+  if (f8) {
+    const int64_t n = (int64_t)T * H * 32 * Npad;
+    RC(ensure(ctx, ctx->tap_v8, (size_t)n));
+    HIPCHK(launch_vt_fp8(vt, ctx->tap_v8.p, n, ctx->stream));
+  }
+  HIPCHK(launch_attn_layer(q, k, vt, out, S, T, H, Npad, N, 0, N, N, S - N, 0, ctx->stream, 0, false,
+                           f8 ? ctx->tap_v8.p : nullptr, f8, base_prec(precision) == PREC_F16));
   return MMPFN_OK;
 }
 
