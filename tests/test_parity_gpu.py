@@ -160,6 +160,7 @@ def _attn_ref(q, k, v):
 
 
 # parity (split bf16), bf16, fp32-input MFMA, fp8 P.V with P e4m3 / e5m2 (V^T e4m3); |O| <= ~1
+# (fp8: x max(1, max |V|) in test_item_attention_layer_fp8; measured max 0.125 at N = 1, |V| <= 3.6)
 ATTN_TOL = {0: 5e-5, 1: 2e-2, 2: 2e-5, 3: 1e-1, 4: 1e-1, 5: 2e-2, 6: 1e-1, 7: 1e-1}
 
 
@@ -285,7 +286,9 @@ def test_item_attention_layer_fp8(S, N, T, prec):
     err = (got.double() - ref).abs().max().item()
     rms = ((got.double() - ref) ** 2).mean().sqrt().item()
     print(f"attention prec {prec} S={S} N={N} T={T}: max {err:.3e} rms {rms:.3e}")
-    assert err < ATTN_TOL[prec]
+    # e4m3 V alone rounds by up to 2^-4 of |V| (N = 1: O = V exactly); the fp8 bands scale with max |V|
+    vmax = v.abs().max().item() if prec in (3, 4, 6, 7) else 1.0
+    assert err < ATTN_TOL[prec] * max(1.0, vmax)
 
 
 @pytest.mark.parametrize("prec", [1, 0, 3, 4, 5])
