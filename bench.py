@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--api-steps", type=int, default=3, help="timed predict_proba calls of the API leg (0: skip)")
     p.add_argument("--no-kv-cache", dest="kv_cache", action="store_false", help="skip the fit_with_cache leg")
     p.add_argument("--no-config-d", dest="config_d", action="store_false", help="skip the config-D leg")
+    p.add_argument("--no-config-e", dest="config_e", action="store_false",
+                   help="skip the config-E leg (fp16 vs the fp8 P.V path)")
     p.add_argument("--no-modality", dest="modality", action="store_false",
                    help="skip the modality-encoder leg (DINOv2 ViT-B/14, ELECTRA-base)")
     p.add_argument("--no-f32", dest="f32_leg", action="store_false", help="skip the fp32 parity-mode leg")
@@ -469,6 +471,65 @@ def config_d_leg(device, world, rank, args, prec):
     }
 
 
+def config_e_leg(device, args):
+    """BASELINE config E: 10 000 support + 2 000 query rows, F = 20, tabular-only, 12 layers (SURVEY 8d seed 4),
+    4 members (feature shuffle + class permutation) through forward_many: the fp16 mode, and the same with the
+    sample-axis attention's P.V on fp8 MFMA (MMPFN_PREC_F16_F8, config E's "fp8 MFMA path").  rows/s =
+    members * (N + Q) / step time; every attention launch also timed by HIP events (mmpfn_kernel_timing)."""
+    import ctypes
+
+    from synth import synth_labels, synth_state_dict, synth_table
+
+    from multimodalpfn_amd import _lib
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+    from multimodalpfn_amd.model.transformer import PerFeatureTransformer
+
+    S, N, F, ncls, seed, M = 12000, 10000, 20, 4, 4, 4
+    cfg = ModelConfig(mgm_heads=8, cap_heads=4)
+    sd = synth_state_dict(state_dict_spec(cfg), seed)
+    model = PerFeatureTransformer(cfg)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    norm = next(e for e in model.encoder if "InputNormalizationEncoderStep" in str(e.__class__))
+    norm.remove_outliers, norm.remove_outliers_sigma = True, 12.0
+    model.to(device)
+    eng = model.engine(device)
+    x = synth_table(S, F, seed, nan_frac=0.01)
+    y = synth_labels(S, ncls, seed)
+    rng = np.random.default_rng(7)
+    items = []
+    for _ in range(M):
+        xm = torch.from_numpy(np.ascontiguousarray(x[:, rng.permutation(F)])).to(device)
+        items.append((xm, None, rng.permutation(ncls)[y[:N].astype(np.int64)].astype(np.float32)))
+    out = {"workload": "config E: N=10000 support + Q=2000 query rows, F=20 tabular, 12 layers, 4 members"}
+    ref = None
+    for name, code in (("f16", _lib.PREC_F16), ("f16 + fp8 P.V (e4m3)", _lib.PREC_F16_F8),
+                       ("f16 + fp8 P.V (e5m2)", _lib.PREC_F16_F8E5), ("bf16", _lib.PREC_BF16)):
+        def step():
+            return eng.forward_many(items, code)
+
+        lg = torch.stack(step())
+        eng.status()
+        k = 3
+        dt = timed_steps(step, k, 1, 1, device)
+        eng.lib.mmpfn_kernel_timing(eng.ctx, 1)
+        timed_steps(step, 1, 0, 1, device)
+        eng.lib.mmpfn_kernel_timing(eng.ctx, 0)
+        ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        eng.lib.mmpfn_kernel_timing_read(eng.ctx, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl))
+        rec = {"value": round(M * S * k / dt, 1), "unit": "rows/s", "ms_per_step": round(dt / k * 1e3, 2),
+               "attention_ms_per_launch": round(ms.value / max(1, n.value), 4),
+               "attention_frac": round(fl.value / (ms.value * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, 4) if n.value else None}
+        if ref is None:
+            ref = lg
+        else:
+            d = (lg - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+            rec["logits_rel_dev_vs_f16"] = float(f"{d:.3e}")
+            rec["argmax_agree_vs_f16"] = round(float((lg.argmax(-1) == ref.argmax(-1)).float().mean()), 4)
+        out[name] = rec
+    eng.close()
+    return out
+
+
 def vit_flops(B, H, W, D=768, depth=12, P=14, cls_only=True) -> float:
     """Executed flops of DINOv2 ViT-B/14 forward_features (the last block on the CLS rows only)."""
     np_ = (H // P) * (W // P)
@@ -672,6 +733,12 @@ def main():
                     k: r[k] for k in ("achieved", "frac", "per_launch_ms")}
     eng.close()
     cfg_d = config_d_leg(device, world, rank, args, prec) if args.config_d else None
+    cfg_e = None
+    if args.config_e and rank == 0:
+        try:
+            cfg_e = config_e_leg(device, args)
+        except Exception as e:  # noqa: BLE001 - reported, the headline number stands on its own
+            cfg_e = {"error": f"{type(e).__name__}: {e}"}
     mod = None
     if args.modality and rank == 0:
         try:
@@ -732,6 +799,7 @@ def main():
             "other_16bit_mode": other16,
             "f32_parity_mode": f32,
             "config_D": cfg_d,
+            "config_E": cfg_e,
             "kv_cache_predict": kv,
             "modality_encoders": mod,
         }

@@ -55,9 +55,9 @@ typedef __attribute__((ext_vector_type(2))) short s16x2;
 // smallest power of two the format still holds (subnormal)
 template <int F8> struct P8;
 #ifndef P8_E4_ETOP
-#define P8_E4_ETOP 2
+#define P8_E4_ETOP 0
 #endif
-template <> struct P8<1> {  // e4m3 (max 448 = 2^8.8): >= 5.8 octaves of headroom, 11 below the first max
+template <> struct P8<1> {  // e4m3 (max 448 = 2^8.8): >= 7.8 octaves of headroom, 9 below the first max
   static constexpr int FMT = 0, ETOP = P8_E4_ETOP, EMIN = -9, EMAX = 8;
   static __device__ __forceinline__ s16x2 cvt(s16x2 old, float a, float b, float sc, bool hi) {
     return hi ? __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(old, a, b, sc, true)

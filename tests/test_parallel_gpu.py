@@ -33,7 +33,7 @@ def _probas(ckdir: Path):
     case = _case(CASE)
     d = case_data(case)
     out = {}
-    for prec, kw in (("f32", {"inference_precision": torch.float32}), ("bf16", {})):
+    for prec, kw in (("f32", {"inference_precision": torch.float32}), ("auto16", {})):
         (ckdir / prec).mkdir(parents=True, exist_ok=True)
         clf = make_classifier(case, write_ckpt(case, ckdir / prec), **kw)
         clf.fit(d["X_train"], d["image_train"], d["y_train"])
@@ -80,7 +80,7 @@ def test_sharded_predict_proba_equals_single_process(tmp_path):
         p.join(timeout=60)
     for rank, got, err in res:
         assert err is None, (rank, err)
-        for prec in ("f32", "bf16"):
+        for prec in ("f32", "auto16"):
             np.testing.assert_array_equal(got[prec], single[prec], err_msg=f"rank {rank} {prec}")
     # every predict split its members over the two ranks (disjoint, complete, both non-empty)
     by_rank = {rank: got["shares"] for rank, got, _ in res}

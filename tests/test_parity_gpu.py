@@ -70,8 +70,10 @@ def test_forward_fp32_input_mfma_mode_matches_reference(case, monkeypatch):
 
 @pytest.mark.parametrize("case", CASES)
 def test_forward_bf16_close_to_reference(case):
+    from multimodalpfn_amd import _lib
+
     z, meta, cfg, sd = load_case(case)
-    out = run_case(z, make_model(cfg, sd), autocast=True)
+    out = run_case(z, make_model(cfg, sd), precision=_lib.PREC_BF16)
     assert np.isfinite(out).all()
     err = rel_err(out, z["logits"])
     print(f"bf16 {case}: rel err {err:.3e}")
@@ -88,6 +90,7 @@ def test_forward_f16_close_to_reference(case):
     model = make_model(cfg, sd)
     out = run_case(z, model, precision=_lib.PREC_F16)
     b16 = run_case(z, model, precision=_lib.PREC_BF16)
+    assert np.array_equal(run_case(z, model, autocast=True), out)  # the reference's autocast = this mode
     assert np.isfinite(out).all()
     err, eb = rel_err(out, z["logits"]), rel_err(b16, z["logits"])
     print(f"f16 {case}: rel err {err:.3e} (bf16 {eb:.3e})")
