@@ -1,4 +1,5 @@
-"""Profiling driver: a few member forwards (bf16; MMPFN_PROF_PREC=f32: the parity mode) at the config-C shape (for rocprofv3 --pmc passes).
+"""Profiling driver: a few member forwards at the config-C shape (for rocprofv3 --pmc passes); MMPFN_PROF_PREC:
+f16 (default, the fp16 mode), bf16, or f32 (the parity mode).
 
 Usage (on the GPU box):  rocprofv3 --pmc <counters> -d <dir> -o run --output-format csv -- \
                               python3 tools/prof_forward.py [n_forwards]
@@ -34,7 +35,7 @@ def main():
     x = torch.from_numpy(synth_table(S, 21, 2, n_cat=18)).cuda()
     im = torch.from_numpy(synth_image(S, 1, 2)).cuda()
     y = synth_labels(S, 6, 2)[:N]
-    prec = _lib.PREC_F32 if os.environ.get("MMPFN_PROF_PREC") == "f32" else _lib.PREC_BF16
+    prec = {"f32": _lib.PREC_F32, "bf16": _lib.PREC_BF16}.get(os.environ.get("MMPFN_PROF_PREC", "f16"), _lib.PREC_F16)
     tok = eng.mixer_tokens(im, prec)
     batch = int(os.environ.get("MMPFN_PROF_BATCH", "1"))  # members per batched forward
     for _ in range(n):
