@@ -73,10 +73,12 @@ struct mmpfn_ctx {
   // parity mode (PREC_F32): every GEMM weight also as bf16 hi | lo planes, keyed by its fp32 copy
   std::map<const void*, DevBuf> split;
   DevBuf enc_w, y_w, y_b, pe_w, pe_b, dec_w1, dec_b1, dec_w2, dec_b2;
+  DevBuf dec_w1_h, dec_w1_f, dec_w2p_h, dec_w2p_f;  // 16-bit decoder: W1 [Fh][E], W2 [16][Fh] permuted
   // mixer
   DevBuf mgm_w1, mgm_w1_h, mgm_b1, mgm_w2, mgm_w2_h, mgm_b2;
   DevBuf cap_qp, cap_kv, cap_kv_h, cap_kv_b, cap_o, cap_o_h, cap_o_b, cap_f0, cap_f0_h, cap_f0_b, cap_f3, cap_f3_h,
       cap_f3_b, cap_ng, cap_nb;
+  DevBuf cap_f0_p, cap_f3_p, cap_vecs;  // E = 192: the FFN in mlp_rows order (bf16) and [bo | b0 | g | b + b3]
   DevBuf moe_w1, moe_w1_h, moe_b1, moe_w2, moe_w2_h, moe_b2, moe_gw, moe_gb;
 
   // workspace of the selected lane (per-member forward state)
@@ -306,6 +308,15 @@ int finalize(mmpfn_ctx* ctx) {
     if ((rc = upload(ctx, ctx->dec_b1, *db1, false))) return rc;
     if ((rc = upload(ctx, ctx->dec_w2, *dw2, false))) return rc;
     if ((rc = upload(ctx, ctx->dec_b2, *db2, false))) return rc;
+    if (d.n_out <= 16 && Fh % 128 == 0 && E % 32 == 0) {
+      std::vector<float> w2p((size_t)16 * Fh, 0.f);
+      std::copy(dw2->begin(), dw2->end(), w2p.begin());
+      w2p = pack_mlp2_perm(w2p, 16, Fh);
+      if ((rc = upload(ctx, ctx->dec_w1_h, *dw1, true))) return rc;
+      if ((rc = upload_f16(ctx, ctx->dec_w1_f, *dw1))) return rc;
+      if ((rc = upload(ctx, ctx->dec_w2p_h, w2p, true))) return rc;
+      if ((rc = upload_f16(ctx, ctx->dec_w2p_f, w2p))) return rc;
+    }
   }
   const int D = d.nhid;
   if (d.mixer_type == MMPFN_MIXER_MGM || d.mixer_type == MMPFN_MIXER_MGM_CAP) {
@@ -394,6 +405,14 @@ int finalize(mmpfn_ctx* ctx) {
     if ((rc = upload(ctx, ctx->cap_f3_b, *f3b, false))) return rc;
     if ((rc = upload(ctx, ctx->cap_ng, *ng, false))) return rc;
     if ((rc = upload(ctx, ctx->cap_nb, *nb, false))) return rc;
+    if (E == 192) {  // the bf16 tail runs on mlp_rows_kernel's CAP form
+      if ((rc = upload(ctx, ctx->cap_f0_p, pack_mlp1_perm(*f0w, E, 2 * E), true))) return rc;
+      if ((rc = upload(ctx, ctx->cap_f3_p, pack_mlp2_perm(*f3w, E, 2 * E), true))) return rc;
+      std::vector<float> v;  // [bo | b0 | g | b + b3]
+      for (const std::vector<float>* part : {ob, f0b, ng}) v.insert(v.end(), part->begin(), part->end());
+      for (int e = 0; e < E; ++e) v.push_back((*nb)[e] + (*f3b)[e]);
+      if ((rc = upload(ctx, ctx->cap_vecs, v, false))) return rc;
+    }
   }
   if (d.mixer_type == MMPFN_MIXER_MOE) {
     const int ne = d.mgm_heads;
@@ -516,20 +535,15 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
       return fail(ctx, MMPFN_ERR_INVALID, "batched members must share S, N, F, C and precision");
     flag = (int*)ctx->ws_flag.p;
   }
-  // PREC_F16: the encoders write fp32 into the attention-output workspace, converted into the fp16 state
+  // the encoders write the state dtype directly (fp16 in PREC_F16)
   const bool h = prec == PREC_F16;
-  float* X = h ? (float*)ctx->ws_O.p + (size_t)m * R * E : (float*)ctx->ws_X.p + (size_t)m * R * E;
-  if (G) {
-    HIPCHK(launch_encode_x(x, S, F, N, G, fpg, d.encoder_features, d.outlier_sigma, (SlotParams*)ctx->ws_slots.p,
-                           (const float*)ctx->enc_w.p, (const float*)ctx->ws_pe.p, X, E, flag, st));
-  }
-  if (C) {
-    HIPCHK(launch_add_tokens(tokens, S, C, (const float*)ctx->ws_pe.p + (size_t)G * E, X + (size_t)G * S * E, E,
-                             flag, st));
-  }
-  HIPCHK(launch_encode_y(y, N, S, uniq, U, (const float*)ctx->y_w.p, (const float*)ctx->y_b.p,
-                         X + (size_t)(T - 1) * S * E, E, (float*)ctx->ws_scr.p, flag, st));
-  if (h) HIPCHK(launch_f32_to_f16(X, 0, (uint16_t*)ctx->ws_X.p + (size_t)m * R * E, 0, (int64_t)R * E, 1, st));
+  void* X = (char*)ctx->ws_X.p + (size_t)m * R * E * (h ? 2 : 4);
+  HIPCHK(launch_encode_stats(x, S, F, N, G, fpg, d.outlier_sigma, (SlotParams*)ctx->ws_slots.p, y, N,
+                             (float*)ctx->ws_scr.p, st));
+  HIPCHK(launch_assemble(x, S, F, G, fpg, d.encoder_features, (const SlotParams*)ctx->ws_slots.p,
+                         (const float*)ctx->enc_w.p, (const float*)ctx->ws_pe.p, tokens, C, y, N, uniq, U,
+                         (const float*)ctx->y_w.p, (const float*)ctx->y_b.p, (const float*)ctx->ws_scr.p, X, h, E, flag,
+                         st));
   ctx->embedded = true;
   return MMPFN_OK;
 }
@@ -555,16 +569,10 @@ int embed_cached(mmpfn_ctx* ctx, const mmpfn_cache* cc, const float* x, int S, i
   RC(ensure(ctx, ctx->ws_big, (R * E + (size_t)2 * S * Tpad * E) * 4));
   RC(ensure_flag(ctx, ctx->ws_flag, st));
   int* flag = (int*)ctx->ws_flag.p;
-  float* X = h ? (float*)ctx->ws_O.p : (float*)ctx->ws_X.p;
-  const float* pe = (const float*)cc->pe.p;
-  if (G)
-    HIPCHK(launch_encode_x(x, S, F, 0, G, fpg, d.encoder_features, d.outlier_sigma, (SlotParams*)cc->slots.p,
-                           (const float*)ctx->enc_w.p, pe, X, E, flag, st, false));
-  if (C) HIPCHK(launch_add_tokens(tokens, S, C, pe + (size_t)G * E, X + (size_t)G * S * E, E, flag, st));
-  HIPCHK(launch_encode_y(nullptr, 0, S, (const float*)cc->uniq.p, cc->U, (const float*)ctx->y_w.p,
-                         (const float*)ctx->y_b.p, X + (size_t)(T - 1) * S * E, E, (float*)cc->ymean.p, flag, st,
-                         false));
-  if (h) HIPCHK(launch_f32_to_f16(X, 0, ctx->ws_X.p, 0, (int64_t)R * E, 1, st));
+  HIPCHK(launch_assemble(x, S, F, G, fpg, d.encoder_features, (const SlotParams*)cc->slots.p,
+                         (const float*)ctx->enc_w.p, (const float*)cc->pe.p, tokens, C, nullptr, 0,
+                         (const float*)cc->uniq.p, cc->U, (const float*)ctx->y_w.p, (const float*)ctx->y_b.p,
+                         (const float*)cc->ymean.p, ctx->ws_X.p, h, E, flag, st));
   ctx->embedded = true;
   return MMPFN_OK;
 }
@@ -815,6 +823,14 @@ int decode(mmpfn_ctx* ctx, float* logits, int M = 1) {
   const size_t off = ((size_t)(T - 1) * S + N) * E;
   const float* Xl = (const float*)ctx->ws_X.p + off;
   int64_t xm = (int64_t)S * T * E;
+  if (prec16(ctx->prec) && ctx->dec_w1_h.p) {  // the state as it is (fp32 / fp16) into 16-bit MFMA operands
+    const bool h = ctx->prec == PREC_F16;
+    const void* X = (const char*)ctx->ws_X.p + off * (h ? 2 : 4);
+    HIPCHK(launch_decoder_mfma(X, h, Q, h ? ctx->dec_w1_f.p : ctx->dec_w1_h.p, (const float*)ctx->dec_b1.p, d.nhid,
+                               h ? ctx->dec_w2p_f.p : ctx->dec_w2p_h.p, (const float*)ctx->dec_b2.p, d.n_out, logits, E,
+                               ctx->stream, M, xm, (int64_t)Q * d.n_out));
+    return MMPFN_OK;
+  }
   if (ctx->prec == PREC_F16) {  // the target token's test rows of every member to fp32 (the big workspace is free)
     RC(ensure(ctx, ctx->ws_big, (size_t)M * Q * E * 4));
     HIPCHK(launch_f16_to_f32((const uint16_t*)ctx->ws_X.p + off, xm, (float*)ctx->ws_big.p, (int64_t)Q * E,
@@ -871,9 +887,12 @@ int mixer_cap(mmpfn_ctx* ctx, const float* mtok, int S, int M, float* tokens, in
   RC(ensure(ctx, ctx->mx[5], (size_t)S * cap * E * 4));       // attention out (heads concat)
   RC(ensure(ctx, ctx->mx[6], (size_t)S * cap * E * 4));       // out_proj
   RC(ensure(ctx, ctx->mx[7], (size_t)S * cap * 2 * E * 4));   // ffn hidden (+ ffn out after)
+  // bf16, E = 192, 24 heads over M % 32 == 0 tokens: K [S*M][E] and V^T [S][E][M] for the MFMA attention
+  const bool mf = bf && E == 192 && cap == 24 && M % 32 == 0 && M <= 128 && ctx->cap_vecs.p;
+  void* vt = (char*)ctx->mx[4].p + (size_t)srows * E * 2;
   if (bf && E == 192) {  // k_norm + K|V projection in one row pass (normalised rows stay in registers)
     HIPCHK(launch_rowgemm_ln_store(mtok, ctx->cap_kv_h.p, (const float*)ctx->cap_kv_b.p, ctx->mx[4].p, srows, 2 * E,
-                                   1e-5f, true, st));
+                                   1e-5f, true, st, mf ? vt : nullptr, E, M));
   } else {
     HIPCHK(launch_layernorm_rows(mtok, srows, E, 1e-5f, ctx->mx[3].p, !bf, nullptr, nullptr, st));
     GemmArgs c = gargs();
@@ -881,9 +900,18 @@ int mixer_cap(mmpfn_ctx* ctx, const float* mtok, int S, int M, float* tokens, in
     c.M = (int)srows, c.N = 2 * E, c.K = E, c.C = ctx->mx[4].p, c.ldc = 2 * E;
     HIPCHK(launch_gemm(c, prec, EPI_STORE, !bf, !bf, 1, st));
   }
-  HIPCHK(launch_cap_attention((const float*)ctx->cap_qp.p, ctx->mx[4].p, !bf, (float*)ctx->mx[5].p, S, M, cap, E,
-                              st));
   const int64_t crow = (int64_t)S * cap;
+  if (bf && E == 192 && ctx->cap_vecs.p) {  // attention out in bf16, then the whole tail in one row-resident pass
+    if (mf)
+      HIPCHK(launch_cap_attention_mfma((const float*)ctx->cap_qp.p, ctx->mx[4].p, vt, ctx->mx[5].p, S, M, cap, E, st));
+    else
+      HIPCHK(launch_cap_attention((const float*)ctx->cap_qp.p, ctx->mx[4].p, false, ctx->mx[5].p, true, S, M, cap, E,
+                                  st));
+    HIPCHK(launch_cap_tail(ctx->mx[5].p, ctx->cap_o_h.p, ctx->cap_f0_p.p, ctx->cap_f3_p.p,
+                           (const float*)ctx->cap_vecs.p, tokens, crow, E, 1e-5f, st));
+    return MMPFN_OK;
+  }
+  HIPCHK(launch_cap_attention((const float*)ctx->cap_qp.p, ctx->mx[4].p, !bf, ctx->mx[5].p, false, S, M, cap, E, st));
   // projections run in fp32 A (tiny); bf16 weights in perf mode
   GemmArgs o = gargs();
   o.A = ctx->mx[5].p, o.lda = E, setw(ctx, o, ctx->cap_o, ctx->cap_o_h, prec), o.bias = (const float*)ctx->cap_o_b.p;
@@ -999,12 +1027,13 @@ void mmpfn_destroy(mmpfn_ctx* ctx) {
                       &L.mlp1_f, &L.mlp2_f})
       fr(*b);
   }
+  for (DevBuf* b : {&ctx->dec_w1_h, &ctx->dec_w1_f, &ctx->dec_w2p_h, &ctx->dec_w2p_f}) fr(*b);
   for (DevBuf* b : {&ctx->enc_w, &ctx->y_w, &ctx->y_b, &ctx->pe_w, &ctx->pe_b, &ctx->dec_w1, &ctx->dec_b1,
                     &ctx->dec_w2, &ctx->dec_b2, &ctx->mgm_w1, &ctx->mgm_w1_h, &ctx->mgm_b1, &ctx->mgm_w2,
                     &ctx->mgm_w2_h, &ctx->mgm_b2, &ctx->cap_qp, &ctx->cap_kv, &ctx->cap_kv_h, &ctx->cap_kv_b,
                     &ctx->cap_o, &ctx->cap_o_h, &ctx->cap_o_b, &ctx->cap_f0, &ctx->cap_f0_h, &ctx->cap_f0_b,
-                    &ctx->cap_f3, &ctx->cap_f3_h, &ctx->cap_f3_b, &ctx->cap_ng, &ctx->cap_nb, &ctx->moe_w1,
-                    &ctx->moe_w1_h, &ctx->moe_b1, &ctx->moe_w2, &ctx->moe_w2_h, &ctx->moe_b2, &ctx->moe_gw,
+                    &ctx->cap_f3, &ctx->cap_f3_h, &ctx->cap_f3_b, &ctx->cap_ng, &ctx->cap_nb, &ctx->cap_f0_p,
+                    &ctx->cap_f3_p, &ctx->cap_vecs, &ctx->moe_w1, &ctx->moe_w1_h, &ctx->moe_b1, &ctx->moe_w2, &ctx->moe_w2_h, &ctx->moe_b2, &ctx->moe_gw,
                     &ctx->moe_gb, &ctx->ws_X, &ctx->ws_O, &ctx->ws_big, &ctx->ws_pe, &ctx->ws_slots, &ctx->ws_scr,
                     &ctx->ws_flag, &ctx->tap_v8, &ctx->tap_x16})
     fr(*b);

@@ -1,13 +1,14 @@
-// Input encoders, positional embedding, token assembly and decoder head (gfx950).
+// Input encoders, positional embedding, state assembly and decoder head (gfx950).
 //
-// x encoder (loading.py:308-371; encoders.py): one block per feature group computes
+// x encoder (loading.py:308-371; encoders.py): one block per (feature group, slot) computes
 // the column statistics the reference fits on the train rows -- constancy over ALL
 // rows (encoders.py:515), NaN/inf fill with the train nanmean (encoders.py:461-493),
 // the two-pass 12-sigma soft outlier bounds (encoders.py:133-162), train z-score
-// (encoders.py:53-99) and the used-feature rescale (encoders.py:608-655).  A second
-// kernel applies them element-wise, embeds with Linear(2*nf -> E) and adds the
-// subspace positional embedding (transformer.py:925-933), writing token g of the
-// [T][S][E] state.  Reductions accumulate in fp64.
+// (encoders.py:53-99) and the used-feature rescale (encoders.py:608-655); one more block of
+// the same launch takes the label mean.  A second kernel writes the member's whole state:
+// the x tokens (statistics applied element-wise, Linear(2*nf -> E), the subspace positional
+// embedding, transformer.py:925-933), the mixer tokens + their positional rows and the label
+// token, in the state dtype.  Reductions accumulate in fp64.
 #include "common.h"
 #include "kernels.h"
 
@@ -27,249 +28,332 @@ __device__ __forceinline__ float soft_clip(float v, float lo, float hi) {
 __device__ __forceinline__ float tmax(float a, float b) { return (isnan(a) || isnan(b)) ? NAN : fmaxf(a, b); }
 __device__ __forceinline__ float tmin(float a, float b) { return (isnan(a) || isnan(b)) ? NAN : fminf(a, b); }
 __device__ __forceinline__ float soft_clip_t(float v, float lo, float hi) {
+  // inside [lo, hi] both steps are the identity (log1p(|v|) >= 0); NaN v / lo / hi take the full form
+  if (v >= lo && v <= hi) return v;
   v = tmax(-logf(1.0f + fabsf(v)) + lo, v);
   v = tmin(logf(1.0f + fabsf(v)) + hi, v);
   return v;
 }
 
+// Reductions of the statistics kernel: a wave sum identical in every lane (each step pairs lanes
+// symmetrically, so both partners add the same two values): DPP quad permutes xor 1 / xor 2, the
+// half-row and row mirrors, then the permlane swaps between the 16-lane rows (no LDS round trips)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+__device__ __forceinline__ double swap_add_d(double v, bool rows32) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const auto a = rows32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                        : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = rows32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                        : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double d0 = __longlong_as_double((long long)(((uint64_t)b[0] << 32) | a[0]));
+  const double d1 = __longlong_as_double((long long)(((uint64_t)b[1] << 32) | a[1]));
+  return d0 + d1;  // {own, partner} in some order: the sum is the same in both lanes
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror
+  v = swap_add_d(v, false);
+  return swap_add_d(v, true);
+}
+// NV sums over a 256-thread block with one barrier; `red` holds two ping-pong sets of 4 * NV doubles (a
+// set is rewritten two reductions later, after every thread has passed the barrier of the one between)
+struct BlockRed {
+  double* red;
+  int k = 0;
+  template <int NV>
+  __device__ __forceinline__ void sum(double (&v)[NV]) {
+    double* r = red + (k & 1) * 32;
+    ++k;
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = wave_sum_dpp(v[i]);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+      for (int i = 0; i < NV; ++i) r[4 * i + w] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = (r[4 * i] + r[4 * i + 1]) + (r[4 * i + 2] + r[4 * i + 3]);
+  }
+};
+
 struct Moments {  // torch_nanmean (clipped count) and torch_nanstd (unbiased)
   float mean_clip, std;
 };
 
-// nan-skipping moments of f(s) over rows [0, n); f returns NaN to skip
-template <typename Fn>
-__device__ Moments nan_moments(int n, Fn f, double* red) {
-  double sum = 0.0, cnt = 0.0;
-  for (int s = threadIdx.x; s < n; s += blockDim.x) {
-    const float v = f(s);
-    if (!isnan(v)) {
-      sum += (double)v;
-      cnt += 1.0;
+// Encoder statistics of one member, one launch: block (g, k) < G * fpg fits slot k of feature group g, the
+// last block the label mean (torch.nanmean of the train labels, the NaN fill of the y encoder).  A slot
+// block stages its group's fpg columns in LDS ([fpg][S], when they fit), finds the group's non-constant
+// columns over all rows (RemoveEmptyFeatures), takes the k-th, and runs the ~9 passes of its statistics:
+// 256 threads, each pass ending in one DPP wave reduction + one barrier.  VPT > 0: the selected column is
+// held in registers (rows tid + 256 i, S <= 256 VPT), so the passes are unrolled register loops.
+template <int VPT>
+__global__ __launch_bounds__(256) void enc_stats_kernel(const float* __restrict__ x, int S, int F, int N, int fpg,
+                                                        int nslots, float sigma, SlotParams* __restrict__ slots,
+                                                        const float* __restrict__ y, int ny, float* __restrict__ ymean,
+                                                        int col_lds) {
+  __shared__ double red[64];
+  extern __shared__ float cols[];  // [fpg][S] when col_lds
+  BlockRed br{red};
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x == nslots) {  // label mean
+    double a[2] = {0.0, 0.0};
+    for (int s = tid; s < ny; s += 256) {
+      const float v = y[s];
+      if (!isnan(v)) a[0] += v, a[1] += 1.0;
     }
+    br.sum(a);
+    if (tid == 0) ymean[0] = (float)(a[0] / a[1]);
+    return;
   }
-  sum = block_sum_d(sum, red);
-  cnt = block_sum_d(cnt, red + 16);
-  const double mu = sum / cnt;  // unclipped (torch_nanstd)
-  double ss = 0.0;
-  for (int s = threadIdx.x; s < n; s += blockDim.x) {
-    const float v = f(s);
-    if (!isnan(v)) {
-      const double dl = mu - (double)v;
-      ss += dl * dl;
-    }
-  }
-  ss = block_sum_d(ss, red + 32);
-  Moments m;
-  m.mean_clip = (float)(sum / (cnt < 1.0 ? 1.0 : cnt));
-  m.std = (float)sqrt(ss / (cnt - 1.0));
-  return m;
-}
-
-// 1024 threads (16 waves): each pass over the rows is two strided loads per thread, so the
-// ~9 dependent passes per column are short; reduction slots of 16 waves at red + {0,16,32}
-__global__ __launch_bounds__(1024) void enc_x_stats_kernel(const float* __restrict__ x, int S, int F, int N, int fpg,
-                                                           int nf, float sigma, SlotParams* __restrict__ slots,
-                                                           int col_lds) {
-  __shared__ double red[48];
-  extern __shared__ float colv[];  // col_lds: the slot's column (S rows) staged once for the ~9 passes
-  __shared__ int s_cnt[8];
-  const int g = blockIdx.x;
-  // 1. constancy over all rows (RemoveEmptyFeatures) for each column of the group
-  int src_of_slot[8];
-  int nsel = 0;
-  for (int j = 0; j < fpg; ++j) {
+  const int g = blockIdx.x / fpg, k = blockIdx.x - g * fpg;
+  auto raw_col = [&](int j, int s) -> float {
     const int c = g * fpg + j;
-    int eq = 0;
-    if (c < F) {
-      const float x0 = x[c];
-      for (int s = 1 + threadIdx.x; s < S; s += blockDim.x) eq += (x[(int64_t)s * F + c] == x0);
-    } else {
-      for (int s = 1 + threadIdx.x; s < S; s += blockDim.x) eq += 1;  // zero padding column
+    if (col_lds) return cols[j * S + s];
+    return c < F ? x[(int64_t)s * F + c] : 0.f;  // zero padding column
+  };
+  if (col_lds) {
+    const int n = S * fpg;
+#pragma unroll 8
+    for (int i = tid; i < n; i += 256) {
+      const int s = i / fpg, j = i - s * fpg, c = g * fpg + j;
+      cols[j * S + s] = c < F ? x[(int64_t)s * F + c] : 0.f;
     }
-    const double tot = block_sum_d((double)eq, red);
-    const bool sel = (int)(tot + 0.5) != S - 1;
-    if (sel) src_of_slot[nsel++] = c;
+    __syncthreads();
   }
-  for (int k = nsel; k < fpg; ++k) src_of_slot[k] = -1;
-
-  // this block's slot (blockIdx.y): the slots of a group are independent once the group's
-  // constant columns are known; the embed kernel sums the groups' used flags
-  {
-    const int k = blockIdx.y;
-    const int c = src_of_slot[k];
-    SlotParams p;
-    p.src = c;
-    p.fill = 0.f;
-    p.lo = -INFINITY;
-    p.hi = INFINITY;
-    p.mean = 0.f;
-    p.sd = 1.f;
-    p.scale = 1.f;
-    if (c >= 0 && col_lds) {
-      for (int s = threadIdx.x; s < S; s += blockDim.x) colv[s] = x[(int64_t)s * F + c];
-      __syncthreads();
+  // 1. constancy over all rows of each column of the group
+  double eq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) eq[j] = 0.0;
+  for (int j = 0; j < fpg; ++j) {
+    const float x0 = raw_col(j, 0);
+    int e = 0;
+    for (int s = 1 + tid; s < S; s += 256) e += raw_col(j, s) == x0;
+    eq[j] = (double)e;
+  }
+  br.sum(eq);
+  int jsel = -1;
+  for (int j = 0, n = 0; j < fpg; ++j)
+    if ((int)(eq[j] + 0.5) != S - 1) {
+      if (n == k) jsel = j;
+      ++n;
     }
-    if (c >= 0) {
-      auto raw = [&](int s) { return col_lds ? colv[s] : x[(int64_t)s * F + c]; };
-      // NaN handling: torch.nanmean over train rows (inf included)
-      {
-        double sum = 0.0, cnt = 0.0;
-        for (int s = threadIdx.x; s < N; s += blockDim.x) {
-          const float v = raw(s);
-          if (!isnan(v)) {
-            sum += (double)v;
-            cnt += 1.0;
-          }
+  SlotParams p;
+  p.src = jsel >= 0 ? g * fpg + jsel : -1;
+  p.fill = 0.f, p.lo = -INFINITY, p.hi = INFINITY, p.mean = 0.f, p.sd = 1.f, p.scale = 0.f;
+  if (jsel >= 0) {  // block-uniform
+    float xv[VPT > 0 ? VPT : 1];
+    if constexpr (VPT > 0) {
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int s = tid + 256 * i;
+        xv[i] = s < S ? raw_col(jsel, s) : 0.f;
+      }
+    }
+    // fn(s, raw value) over rows [r0, n) of this thread
+    auto for_rows = [&](int r0, int n, auto&& fn) __attribute__((always_inline)) {
+      if constexpr (VPT > 0) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+          const int s = tid + 256 * i;
+          if (s >= r0 && s < n) fn(xv[i]);
         }
-        sum = block_sum_d(sum, red);
-        cnt = block_sum_d(cnt, red + 16);
-        p.fill = (float)(sum / cnt);
+      } else {
+        for (int s = r0 + tid; s < n; s += 256) fn(raw_col(jsel, s));
       }
-      const float fill = p.fill;
-      auto filled = [&](int s) {
-        const float v = raw(s);
-        return bad(v) ? fill : v;
-      };
-      if (sigma > 0.f) {
-        const Moments a = nan_moments(N, filled, red);
-        const float lo1 = a.mean_clip - a.std * sigma, hi1 = a.mean_clip + a.std * sigma;
-        auto cleaned = [&](int s) {
-          const float v = filled(s);
-          return (v > hi1 || v < lo1) ? NAN : v;
-        };
-        const Moments b = nan_moments(N, cleaned, red);
-        p.lo = b.mean_clip - b.std * sigma;
-        p.hi = b.mean_clip + b.std * sigma;
-      }
-      const float lo = p.lo, hi = p.hi;
-      const bool clipping = sigma > 0.f;
-      auto clipped = [&](int s) {
-        const float v = filled(s);
-        return clipping ? soft_clip_t(v, lo, hi) : v;
-      };
-      const Moments nm = nan_moments(N, clipped, red);
-      p.mean = nm.mean_clip;
-      p.sd = (S == 1 || N == 1) ? 1.0f : nm.std + 1e-20f;
-      // used-feature test on the normalised values over all rows
-      const float mean = p.mean, sd = p.sd;
-      auto normed = [&](int s) { return tmin(tmax((clipped(s) - mean) / sd, -100.f), 100.f); };
-      const float u0 = normed(0);
-      int eq = 0;
-      for (int s = 1 + threadIdx.x; s < S; s += blockDim.x) eq += (normed(s) == u0);
-      const double tot = block_sum_d((double)eq, red);
-      p.scale = (int)(tot + 0.5) != S - 1 ? 1.f : 0.f;  // used flag; the embed kernel rescales
-    } else {
-      p.scale = 0.f;
+    };
+    // nan-skipping moments of f(raw) over rows [0, N); f returns NaN to skip
+    auto moments = [&](auto&& f) __attribute__((always_inline)) {
+      double a[2] = {0.0, 0.0};  // sum, count
+      for_rows(0, N, [&](float r) {
+        const float v = f(r);
+        if (!isnan(v)) a[0] += (double)v, a[1] += 1.0;
+      });
+      br.sum(a);
+      const double mu = a[0] / a[1];  // unclipped (torch_nanstd)
+      double ss[1] = {0.0};
+      for_rows(0, N, [&](float r) {
+        const float v = f(r);
+        if (!isnan(v)) {
+          const double dl = mu - (double)v;
+          ss[0] += dl * dl;
+        }
+      });
+      br.sum(ss);
+      Moments m;
+      m.mean_clip = (float)(a[0] / (a[1] < 1.0 ? 1.0 : a[1]));
+      m.std = (float)sqrt(ss[0] / (a[1] - 1.0));
+      return m;
+    };
+    {  // NaN handling: torch.nanmean over train rows (inf included)
+      double a[2] = {0.0, 0.0};
+      for_rows(0, N, [&](float v) {
+        if (!isnan(v)) a[0] += (double)v, a[1] += 1.0;
+      });
+      br.sum(a);
+      p.fill = (float)(a[0] / a[1]);
     }
-    if (threadIdx.x == 0) slots[g * fpg + k] = p;
+    const float fill = p.fill;
+    auto filled = [&](float v) { return bad(v) ? fill : v; };
+    if (sigma > 0.f) {
+      const Moments a = moments(filled);
+      const float lo1 = a.mean_clip - a.std * sigma, hi1 = a.mean_clip + a.std * sigma;
+      const Moments b = moments([&](float r) {
+        const float v = filled(r);
+        return (v > hi1 || v < lo1) ? NAN : v;
+      });
+      p.lo = b.mean_clip - b.std * sigma;
+      p.hi = b.mean_clip + b.std * sigma;
+    }
+    const float lo = p.lo, hi = p.hi;
+    const bool clipping = sigma > 0.f;
+    auto clipped = [&](float r) {
+      const float v = filled(r);
+      return clipping ? soft_clip_t(v, lo, hi) : v;
+    };
+    const Moments nm = moments(clipped);
+    p.mean = nm.mean_clip;
+    p.sd = (S == 1 || N == 1) ? 1.0f : nm.std + 1e-20f;
+    // used-feature test on the normalised values over all rows
+    const float mean = p.mean, sd = p.sd;
+    auto normed = [&](float r) { return tmin(tmax((clipped(r) - mean) / sd, -100.f), 100.f); };
+    const float u0 = normed(raw_col(jsel, 0));
+    int e = 0;
+    for_rows(1, S, [&](float r) { e += (normed(r) == u0); });
+    double tot[1] = {(double)e};
+    br.sum(tot);
+    p.scale = (int)(tot[0] + 0.5) != S - 1 ? 1.f : 0.f;  // used flag; the assembly rescales
   }
-  (void)s_cnt;
+  if (tid == 0) slots[blockIdx.x] = p;
 }
 
-// EMB_TOK tokens per block: the per-token model inputs (u, NaN/inf indicators) are computed
-// once per (token, slot) into LDS next to the encoder weights; then each thread writes 16-B
-// pieces of the embedding (4 columns of one token, consecutive threads -> consecutive columns),
-// adding the token's group positional row straight from global memory (one 768-B row per group,
-// cache resident).  16 tokens per block (64 measured 31 vs 33 us alone but 53 vs 46 us beside the
-// other lane's kernels in the bench: small blocks share the CUs better).
-constexpr int EMB_TOK = 16;
+// The member's whole input state X [T][S][E] in one launch, written in the state dtype TX (fp32, or fp16 in
+// PREC_F16): rows t < G are the x encoder's tokens (the statistics applied element-wise, Linear(2 nf -> E)
+// and the group's positional row; transformer.py:925-933), G <= t < G + C the mixer tokens + their
+// positional rows, t = T - 1 the label token (encoders.py target encoder; NaN labels -> train mean,
+// indicator -2).  ASM_ROWS rows per block: the per-row encoder inputs (u, NaN / inf indicator; label
+// class and indicator) go to LDS once, then each thread writes 16-B pieces of the rows.
+constexpr int ASM_ROWS = 32;
 constexpr int EMB_EMAX = 256;
-__global__ __launch_bounds__(256) void enc_x_embed_kernel(const float* __restrict__ x, int S, int F, int G, int fpg,
-                                                          int nf, const SlotParams* __restrict__ slots,
-                                                          const float* __restrict__ w, const float* __restrict__ pe,
-                                                          float* __restrict__ X, int E, int* flag) {
-  __shared__ float su[EMB_TOK][8], si[EMB_TOK][8];
-  __shared__ float ws[EMB_EMAX * 16];
-  const int tid = threadIdx.x, nin = 2 * nf;
-  const int64_t ntok = (int64_t)S * G, tok0 = (int64_t)blockIdx.x * EMB_TOK;
-  for (int i = tid; i < E * nin; i += blockDim.x) ws[i] = w[i];
-  for (int it = tid; it < EMB_TOK * 8; it += blockDim.x) {
-    const int i = it >> 3, k = it & 7;
-    const int64_t tok = tok0 + i;
+struct AsmArgs {
+  const float* x;
+  int S, F, G, fpg, nf;
+  const SlotParams* slots;
+  const float* w_enc;  // [E][2 nf]
+  const float* pe;     // [G + C][E]
+  const float* tok;    // [S][C][E]
+  int C;
+  const float* y;  // [N] train labels (rows >= N: test rows)
+  int N;
+  const float* uniq;
+  int U;
+  const float *yw, *yb, *ymean;
+  void* X;
+  int E;
+  int* flag;
+};
+template <typename TX>
+__global__ __launch_bounds__(256) void assemble_kernel(const AsmArgs a) {
+  __shared__ float su[ASM_ROWS][8], si[ASM_ROWS][8];
+  __shared__ __attribute__((aligned(16))) float ws[EMB_EMAX * 16];  // [2 nf][E]: a piece's weights are 16-B runs
+  const int tid = threadIdx.x, S = a.S, G = a.G, C = a.C, T = G + C + 1, E = a.E, nf = a.nf, fpg = a.fpg;
+  const int nrows = T * S, r0 = blockIdx.x * ASM_ROWS;
+  const int rn = min(ASM_ROWS, nrows - r0);
+  const bool xrows = r0 / S < G;
+  if (xrows)
+    for (int i = tid; i < E * 2 * nf; i += 256) {
+      const int e = i / (2 * nf), k = i - e * 2 * nf;
+      ws[k * E + e] = a.w_enc[i];
+    }
+  for (int it = tid; it < rn * 8; it += 256) {
+    const int i = it >> 3, k = it & 7, r = r0 + i, t = r / S, s = r - t * S;
     float u = 0.f, ind = 0.f;
-    if (tok < ntok && k < fpg) {
-      const int g = (int)tok / S, s = (int)tok - g * S;
-      const SlotParams p = slots[g * fpg + k];
-      float used = 0.f;  // used-feature rescale sqrt(nf / used) of the group (encoders.py:608-655)
-      for (int j = 0; j < fpg; ++j) used += slots[g * fpg + j].scale;
-      const float scale = sqrtf((float)nf / fmaxf(used, 1.f));
-      if (p.src >= 0) {
-        const float raw = x[(int64_t)s * F + p.src];
-        ind = isnan(raw) ? -2.0f : (isinf(raw) ? (raw > 0 ? 2.0f : 4.0f) : 0.0f);
-        float v = bad(raw) ? p.fill : raw;
-        v = soft_clip_t(v, p.lo, p.hi);
-        v = tmin(tmax((v - p.mean) / p.sd, -100.f), 100.f);
-        u = v * scale;
+    if (t < G) {
+      if (k < fpg) {
+        const SlotParams p = a.slots[t * fpg + k];
+        float used = 0.f;  // used-feature rescale sqrt(nf / used) of the group (encoders.py:608-655)
+        for (int j = 0; j < fpg; ++j) used += a.slots[t * fpg + j].scale;
+        const float scale = sqrtf((float)nf / fmaxf(used, 1.f));
+        if (p.src >= 0) {
+          const float raw = a.x[(int64_t)s * a.F + p.src];
+          ind = isnan(raw) ? -2.0f : (isinf(raw) ? (raw > 0 ? 2.0f : 4.0f) : 0.0f);
+          float v = bad(raw) ? p.fill : raw;
+          v = soft_clip_t(v, p.lo, p.hi);
+          v = tmin(tmax((v - p.mean) / p.sd, -100.f), 100.f);
+          u = v * scale;
+        }
       }
+    } else if (t == T - 1 && k == 0) {
+      float yv = s < a.N ? a.y[s] : NAN;
+      ind = isnan(yv) ? -2.0f : 0.0f;
+      if (isnan(yv)) yv = a.ymean[0];
+      for (int i2 = 0; i2 < a.U; ++i2) u += (yv > a.uniq[i2]) ? 1.f : 0.f;
     }
     su[i][k] = u, si[i][k] = ind;
   }
   __syncthreads();
-  const int E4 = E / 4;
-  bool nan_seen = false;
-  for (int item = tid; item < EMB_TOK * E4; item += blockDim.x) {
-    const int i = item / E4, e4 = item - i * E4;
-    const int64_t tok = tok0 + i;
-    if (tok >= ntok) break;
-    const f32x4 pv = *(const f32x4*)(pe + (int)((int)tok / S) * E + e4 * 4);  // S * G < 2^31 (launcher)
-    f32x4 o;
+  constexpr int PE = 16 / sizeof(TX);  // elements per 16-B piece
+  const int npc = E / PE;
+  bool nan_x = false, nan_y = false;
+  for (int item = tid; item < rn * npc; item += 256) {
+    const int i = item / npc, e0 = (item - i * npc) * PE, r = r0 + i, t = r / S, s = r - t * S;
+    float o[PE];
+    if (t < G) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int e = e4 * 4 + c;
-      const float* wr = ws + e * nin;
-      float a = 0.f;
-      for (int k = 0; k < nf; ++k) a = fmaf(su[i][k], wr[k], a);
-      for (int k = 0; k < nf; ++k) a = fmaf(si[i][k], wr[nf + k], a);
-      a += pv[c];
-      o[c] = a;
-      nan_seen |= isnan(a);
-    }
-    *(f32x4*)(X + tok * E + e4 * 4) = o;
-  }
-  if (nan_seen) atomicOr(flag, 1);
-}
-
-__global__ void y_stats_kernel(const float* __restrict__ y, int N, float* out) {
-  __shared__ double red[16];
-  double sum = 0.0, cnt = 0.0;
-  for (int s = threadIdx.x; s < N; s += blockDim.x) {
-    const float v = y[s];
-    if (!isnan(v)) {
-      sum += v;
-      cnt += 1.0;
-    }
-  }
-  sum = block_sum_d(sum, red);
-  cnt = block_sum_d(cnt, red + 4);
-  if (threadIdx.x == 0) out[0] = (float)(sum / cnt);
-}
-
-__global__ __launch_bounds__(256) void enc_y_embed_kernel(const float* __restrict__ y, int N, int S,
-                                                          const float* __restrict__ uniq, int U,
-                                                          const float* __restrict__ w, const float* __restrict__ b,
-                                                          const float* __restrict__ ymean, float* __restrict__ Xy,
-                                                          int E, int* flag) {
-  const int E4 = E / 4;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)S * E4) return;
-  const int e4 = idx % E4;
-  const int s = idx / E4;
-  float yv = s < N ? y[s] : NAN;
-  const float ind = isnan(yv) ? -2.0f : 0.0f;
-  if (isnan(yv)) yv = ymean[0];
-  float yc = 0.f;
-  for (int i = 0; i < U; ++i) yc += (yv > uniq[i]) ? 1.f : 0.f;
-  f32x4 o;
-  bool nan_seen = false;
+      for (int c = 0; c < PE; ++c) o[c] = 0.f;
+      for (int k = 0; k < nf; ++k) {
+        const float u = su[i][k];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int e = e4 * 4 + i;
-    const float a = fmaf(ind, w[e * 2 + 1], yc * w[e * 2]) + b[e];
-    o[i] = a;
-    nan_seen |= isnan(a);
+        for (int c = 0; c < PE; ++c) o[c] = fmaf(u, ws[k * E + e0 + c], o[c]);
+      }
+      for (int k = 0; k < nf; ++k) {
+        const float u = si[i][k];
+#pragma unroll
+        for (int c = 0; c < PE; ++c) o[c] = fmaf(u, ws[(nf + k) * E + e0 + c], o[c]);
+      }
+      const float* pr = a.pe + t * E + e0;
+#pragma unroll
+      for (int c = 0; c < PE; ++c) {
+        o[c] += pr[c];
+        nan_x |= isnan(o[c]);
+      }
+    } else if (t < G + C) {
+      const float* tr = a.tok + ((int64_t)s * C + (t - G)) * E + e0;
+#pragma unroll
+      for (int c = 0; c < PE; c += 4) {
+        const f32x4 v = *(const f32x4*)(tr + c) + *(const f32x4*)(a.pe + t * E + e0 + c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[c + q] = v[q], nan_x |= isnan(v[q]);
+      }
+    } else {
+      const float yc = su[i][0], ind = si[i][0];
+#pragma unroll
+      for (int c = 0; c < PE; ++c) {
+        const int e = e0 + c;
+        o[c] = fmaf(ind, a.yw[e * 2 + 1], yc * a.yw[e * 2]) + a.yb[e];
+        nan_y |= isnan(o[c]);
+      }
+    }
+    TX* dst = (TX*)a.X + (int64_t)r * E + e0;
+    if constexpr (PE == 4) {
+      *(f32x4*)dst = f32x4{o[0], o[1], o[2], o[3]};
+    } else {
+      f16x8 h;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) h[c] = (f16)o[c];
+      *(f16x8*)dst = h;
+    }
   }
-  *(f32x4*)(Xy + (int64_t)s * E + e4 * 4) = o;
-  if (nan_seen) atomicOr(flag, 2);
+  if (nan_x) atomicOr(a.flag, 1);
+  if (nan_y) atomicOr(a.flag, 2);
 }
 
 __global__ void pos_emb_kernel(const float* __restrict__ rnd, int n, const float* __restrict__ w,
@@ -281,22 +365,6 @@ __global__ void pos_emb_kernel(const float* __restrict__ rnd, int n, const float
   float a = 0.f;
   for (int j = 0; j < D; ++j) a = fmaf(rnd[k * D + j], w[e * D + j], a);
   out[idx] = a + b[e];
-}
-
-__global__ __launch_bounds__(256) void add_tokens_kernel(const float* __restrict__ tok, int S, int C,
-                                                         const float* __restrict__ pe, float* __restrict__ X, int E,
-                                                         int* flag) {
-  const int E4 = E / 4;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)S * C * E4) return;
-  const int e4 = idx % E4;
-  const int64_t r = idx / E4;  // r = c*S + s  (output order)
-  const int s = r % S, c = r / S;
-  f32x4 v = *(const f32x4*)(tok + ((int64_t)s * C + c) * E + e4 * 4);
-  const f32x4 p = *(const f32x4*)(pe + (int64_t)c * E + e4 * 4);
-  v += p;
-  *(f32x4*)(X + ((int64_t)c * S + s) * E + e4 * 4) = v;
-  if (isnan(v[0]) || isnan(v[1]) || isnan(v[2]) || isnan(v[3])) atomicOr(flag, 1);
 }
 
 // Decoder (transformer.py:388-403,850-853): out = GELU(X W1^T + b1) W2^T + b2 over the Q test rows
@@ -369,6 +437,71 @@ __global__ __launch_bounds__(256) void dec_sum_kernel(const float* __restrict__ 
   out[m * om + k] = a;
 }
 
+// Decoder of the 16-bit modes on MFMA (the reference runs it under its fp16 autocast): one block per 16
+// query rows of one member, wave w owning hidden units [w Fh / 4, (w + 1) Fh / 4):
+//   H^T = W1 X^T on v_mfma_f32_16x16x32 (A: W1 rows from L2, B: the rows' X fragments, the fp32 state
+//   rounded / the fp16 state as is), + b1, exact-erf GELU;
+//   out^T = W2p G^T with G^T straight from the H^T accumulators (W2's hidden order permuted as the MLP's,
+//   weight_pack.h pack_mlp2_perm; outputs padded to 16 rows), the four waves' partial sums added in LDS.
+template <typename TX>
+__global__ __launch_bounds__(256) void dec_mfma_kernel(const TX* __restrict__ X, int Q, int64_t xm,
+                                                       const void* __restrict__ W1v, const float* __restrict__ b1,
+                                                       int Fh, const void* __restrict__ W2v,
+                                                       const float* __restrict__ b2, int n_out, float* __restrict__ out,
+                                                       int64_t om, int E) {
+  constexpr bool F16 = sizeof(TX) == 2;
+  typedef typename Op16<F16>::t HT;
+  typedef typename Op16<F16>::x8 X8;
+  __shared__ f32x4 part[4][64];
+  const HT* W1 = (const HT*)W1v;
+  const HT* W2 = (const HT*)W2v;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
+  const int m = blockIdx.y, q0 = blockIdx.x * 16;
+  const TX* xr = X + m * xm + (int64_t)min(q0 + fr, Q - 1) * E + 8 * fg;
+  const int hw = Fh / 4, h0 = wave * hw;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};  // out^T tile: lane (row fr, outputs 4 fg + i)
+  for (int hc = 0; hc < hw; hc += 32) {  // 32 hidden units: tiles t = 0, 1
+    f32x4 h[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int ks = 0; ks < E / 32; ++ks) {
+      X8 xb;
+      if constexpr (F16) {
+        xb = *(const X8*)(xr + 32 * ks);
+      } else {
+        const f32x4 a = *(const f32x4*)(xr + 32 * ks), b = *(const f32x4*)(xr + 32 * ks + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xb[j] = (HT)a[j], xb[4 + j] = (HT)b[j];
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const X8 wa = *(const X8*)(W1 + (int64_t)(h0 + hc + 16 * t + fr) * E + 32 * ks + 8 * fg);
+        h[t] = mfma16x(wa, xb, h[t]);
+      }
+    }
+    // G^T fragment: lane (row fr, fg) <- hidden hc + 16 (j / 4) + 4 fg + j % 4 (the pack_mlp2_perm order)
+    X8 gb;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int hid = h0 + hc + 16 * t + 4 * fg + i;
+        gb[4 * t + i] = (HT)gelu_erf(h[t][i] + b1[hid]);
+      }
+    const X8 wb = *(const X8*)(W2 + (int64_t)fr * Fh + h0 + hc + 8 * fg);
+    acc = mfma16x(wb, gb, acc);
+  }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0) {
+    const f32x4 s = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    if (q0 + fr < Q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = 4 * fg + i;
+        if (o < n_out) out[m * om + (int64_t)(q0 + fr) * n_out + o] = s[i] + b2[o];
+      }
+  }
+}
+
 // ensemble aggregation (classifier.py:541-566): per query row, per member
 // logits[:, :n_cls] / T (if T != 1) -> class-permutation undo -> softmax -> mean
 // (or mean -> softmax), optional class re-weighting, renormalise.
@@ -436,29 +569,46 @@ hipError_t launch_aggregate(const float* logits, int M, int Q, int n_out, const 
   return hipGetLastError();
 }
 
-hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, int nf, float sigma,
-                           SlotParams* slots, const float* w_enc, const float* posemb, float* X, int E, int* flag,
-                           hipStream_t st, bool stats) {
-  if (G <= 0) return hipSuccess;
-  if (fpg > 8 || nf > 8 || nf < fpg) return hipErrorInvalidValue;
-  if (stats) {
-    const int col_lds = (size_t)S * sizeof(float) <= 48 * 1024 ? 1 : 0;  // stage the column when it fits
-    hipLaunchKernelGGL(enc_x_stats_kernel, dim3(G, fpg), dim3(1024), col_lds ? (size_t)S * sizeof(float) : 0, st, x, S,
-                       F, N, fpg, nf, sigma, slots, col_lds);
+hipError_t launch_encode_stats(const float* x, int S, int F, int N, int G, int fpg, float sigma, SlotParams* slots,
+                               const float* y, int ny, float* ymean, hipStream_t st) {
+  if (G < 0 || S <= 0 || (G > 0 && (fpg <= 0 || fpg > 8 || !x)) || !y || !ymean) return hipErrorInvalidValue;
+  const int nslots = G * fpg;
+  const size_t cb = (size_t)S * fpg * sizeof(float);
+  const int col_lds = G > 0 && cb <= 128 * 1024 ? 1 : 0;  // stage the group's columns when they fit
+  const size_t lds = col_lds ? cb : 0;
+  if (lds > 64 * 1024) {
+    static std::atomic<uint64_t> opted16{0}, opted0{0};
+    const hipError_t e = S <= 256 * 16 ? lds_optin(opted16, (const void*)enc_stats_kernel<16>, 128 * 1024)
+                                       : lds_optin(opted0, (const void*)enc_stats_kernel<0>, 128 * 1024);
+    if (e != hipSuccess) return e;
   }
-  if (fpg > 8 || nf > 8 || E > EMB_EMAX || E % 4 != 0 || (int64_t)S * G >= INT32_MAX) return hipErrorInvalidValue;
-  const int64_t nblk = ((int64_t)S * G + EMB_TOK - 1) / EMB_TOK;
-  hipLaunchKernelGGL(enc_x_embed_kernel, dim3((unsigned)nblk), dim3(256), 0, st, x, S, F, G, fpg, nf, slots, w_enc,
-                     posemb, X, E, flag);
+  const dim3 grid((unsigned)(nslots + 1));
+  if (S <= 256 * 16)
+    hipLaunchKernelGGL((enc_stats_kernel<16>), grid, dim3(256), lds, st, x, S, F, N, fpg, nslots, sigma, slots, y, ny,
+                       ymean, col_lds);
+  else
+    hipLaunchKernelGGL((enc_stats_kernel<0>), grid, dim3(256), lds, st, x, S, F, N, fpg, nslots, sigma, slots, y, ny,
+                       ymean, col_lds);
   return hipGetLastError();
 }
 
-hipError_t launch_encode_y(const float* y_train, int N, int S, const float* uniq, int U, const float* w,
-                           const float* b, float* Xy, int E, float* scratch, int* flag, hipStream_t st, bool stats) {
-  if (stats) hipLaunchKernelGGL(y_stats_kernel, dim3(1), dim3(256), 0, st, y_train, N, scratch);
-  const int64_t n = (int64_t)S * (E / 4);
-  hipLaunchKernelGGL(enc_y_embed_kernel, dim3((n + 255) / 256), dim3(256), 0, st, y_train, N, S, uniq, U, w, b,
-                     scratch, Xy, E, flag);
+hipError_t launch_assemble(const float* x, int S, int F, int G, int fpg, int nf, const SlotParams* slots,
+                           const float* w_enc, const float* posemb, const float* tok, int C, const float* y, int N,
+                           const float* uniq, int U, const float* yw, const float* yb, const float* ymean, void* X,
+                           bool half, int E, int* flag, hipStream_t st) {
+  if (S <= 0 || G < 0 || C < 0 || U < 0 || N < 0 || N > S) return hipErrorInvalidValue;
+  if ((G > 0 && (!x || !slots || fpg <= 0 || fpg > 8 || nf > 8 || nf < fpg)) || (C > 0 && !tok) || (N > 0 && !y))
+    return hipErrorInvalidValue;
+  if (E > EMB_EMAX || E % (half ? 8 : 4) != 0 || (int64_t)(G + C + 1) * S >= INT32_MAX / 2) return hipErrorInvalidValue;
+  AsmArgs a;
+  a.x = x, a.S = S, a.F = F, a.G = G, a.fpg = fpg, a.nf = nf, a.slots = slots, a.w_enc = w_enc, a.pe = posemb;
+  a.tok = tok, a.C = C, a.y = y, a.N = N, a.uniq = uniq, a.U = U, a.yw = yw, a.yb = yb, a.ymean = ymean;
+  a.X = X, a.E = E, a.flag = flag;
+  const int nb = (int)(((int64_t)(G + C + 1) * S + ASM_ROWS - 1) / ASM_ROWS);
+  if (half)
+    hipLaunchKernelGGL((assemble_kernel<f16>), dim3(nb), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((assemble_kernel<float>), dim3(nb), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -466,14 +616,6 @@ hipError_t launch_pos_emb(const float* rnd, int n, const float* w, const float* 
                           hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(pos_emb_kernel, dim3((n * E + 255) / 256), dim3(256), 0, st, rnd, n, w, b, out, E);
-  return hipGetLastError();
-}
-
-hipError_t launch_add_tokens(const float* tok, int S, int C, const float* posemb, float* X, int E, int* flag,
-                             hipStream_t st) {
-  if (C <= 0) return hipSuccess;
-  const int64_t n = (int64_t)S * C * (E / 4);
-  hipLaunchKernelGGL(add_tokens_kernel, dim3((n + 255) / 256), dim3(256), 0, st, tok, S, C, posemb, X, E, flag);
   return hipGetLastError();
 }
 
@@ -490,6 +632,21 @@ hipError_t launch_decoder(const float* X, int Q, const float* w1t, const float* 
   const int64_t n = (int64_t)M * Q * n_out;
   hipLaunchKernelGGL(dec_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, scratch, M, Q, nt, n_out, b2,
                      out, om);
+  return hipGetLastError();
+}
+
+hipError_t launch_decoder_mfma(const void* X, bool x_f16, int Q, const void* W1, const float* b1, int Fh, const void* W2p,
+                               const float* b2, int n_out, float* out, int E, hipStream_t st, int M, int64_t xm,
+                               int64_t om) {
+  if (Q <= 0 || M <= 0) return hipSuccess;
+  if (E % 32 != 0 || Fh % 128 != 0 || n_out > 16 || n_out <= 0) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((Q + 15) / 16), (unsigned)M);
+  if (x_f16)
+    hipLaunchKernelGGL((dec_mfma_kernel<f16>), grid, dim3(256), 0, st, (const f16*)X, Q, xm, W1, b1, Fh, W2p, b2, n_out,
+                       out, om, E);
+  else
+    hipLaunchKernelGGL((dec_mfma_kernel<float>), grid, dim3(256), 0, st, (const float*)X, Q, xm, W1, b1, Fh, W2p, b2,
+                       n_out, out, om, E);
   return hipGetLastError();
 }
 

@@ -419,7 +419,10 @@ hipError_t launch_e(const GemmArgs& a, int epi, int groups, hipStream_t st) {
 constexpr int GB_M = 256, GB_N = 256, GB_K = 32;
 constexpr int GB_ROW = GB_K * 2;                    // 64-B LDS rows
 constexpr int GB_STAGE = (GB_M + GB_N) * GB_ROW;    // 32 KB
-constexpr int GB_NST = 4;                           // ring stages (128 KB)
+#ifndef GB_STAGES
+#define GB_STAGES 4
+#endif
+constexpr int GB_NST = GB_STAGES;                   // ring stages (128 KB)
 constexpr int GB_OST = GB_N / 2 + 8;                // output staging row stride (bf16)
 constexpr int GB_DMA = (GB_M + GB_N) * (GB_ROW / 16) / 512;  // 16-B DMA pieces per thread and slice (4)
 constexpr int GB_MT = GB_M / 32;                    // 16-row MFMA tiles per wave (8)
@@ -478,7 +481,8 @@ __global__ __launch_bounds__(512, 1) void gemm_glu_big_kernel(const bf16* __rest
   for (int kt = 0; kt < nk; ++kt) {
     // this thread's pieces of slice kt have landed (up to two later slices may still fly)
     const int ahead = min(nk - 1 - kt, GB_NST - 2);
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GB_DMA) : "memory");
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GB_DMA) : "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GB_DMA) : "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB_DMA) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

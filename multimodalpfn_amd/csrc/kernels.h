@@ -113,9 +113,12 @@ hipError_t launch_rowgemm_qkv_pair(const void* X, int64_t rdiv1, int64_t roff1, 
                                    int64_t rdiv2, int64_t roff2, const void* W2, int M2, int N2, int64_t a_rmul,
                                    void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st,
                                    bool f16 = false);
-// C = (ln ? LayerNorm(A) : A) . W^T + bias: A fp32 [M][192], W [N][192] bf16, C bf16 [M][N], N % 64 == 0
+// C = (ln ? LayerNorm(A) : A) . W^T + bias: A fp32 [M][192], W [N][192] bf16, C bf16 [M][N], N % 64 == 0;
+// with CT: outputs [vt_from, N) transposed per group of Mk rows into CT [M / Mk][N - vt_from][Mk] (Mk % 32 == 0),
+// C then [M][vt_from]
 hipError_t launch_rowgemm_ln_store(const float* A, const void* W, const float* bias, void* C, int64_t M, int N,
-                                   float eps, bool ln, hipStream_t st);
+                                   float eps, bool ln, hipStream_t st, void* CT = nullptr, int vt_from = -1,
+                                   int Mk = 0);
 hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, void* X, float eps, hipStream_t st,
                                 bool f16 = false);
 
@@ -216,22 +219,29 @@ struct SlotParams {  // per (group, slot): how to transform raw column -> model 
   float mean, sd;    // train z-score (sd already includes the +1e-20)
   float scale;       // 1 if the slot's column is used (non-constant after normalisation), else 0
 };
-hipError_t launch_encode_x(const float* x, int S, int F, int N, int G, int fpg, int nf, float sigma,
-                           SlotParams* slots, const float* w_enc /*[E][2nf]*/, const float* posemb,
-                           float* X /*[T][S][E]*/, int E, int* flag, hipStream_t st, bool stats = true);
-hipError_t launch_encode_y(const float* y_train, int N, int S, const float* uniq, int U,
-                           const float* w /*[E][2]*/, const float* b, float* Xy /*[S][E]*/, int E,
-                           float* scratch, int* flag, hipStream_t st, bool stats = true);
-// stats = false: slots / scratch[0] already hold the train statistics (train-KV cache predict)
+// encoder statistics of one member: x-encoder slots [G * fpg] (train rows [0, N) of S) and the label mean
+// ymean[0] over y[0, ny), one launch
+hipError_t launch_encode_stats(const float* x /*[S][F]*/, int S, int F, int N, int G, int fpg, float sigma,
+                               SlotParams* slots, const float* y, int ny, float* ymean, hipStream_t st);
+// the member's input state X [T][S][E] (T = G + C + 1), fp32 or fp16 (f16): x tokens from the slots, mixer
+// tokens + positional rows, the label token (labels y[0, N); rows >= N are test rows); NaN -> flag bits 1 / 2
+hipError_t launch_assemble(const float* x, int S, int F, int G, int fpg, int nf, const SlotParams* slots,
+                           const float* w_enc /*[E][2nf]*/, const float* posemb /*[G+C][E]*/,
+                           const float* tok /*[S][C][E]*/, int C, const float* y, int N, const float* uniq, int U,
+                           const float* yw /*[E][2]*/, const float* yb, const float* ymean, void* X, bool f16, int E,
+                           int* flag, hipStream_t st);
 hipError_t launch_pos_emb(const float* rnd /*[n][E/4]*/, int n, const float* w /*[E][E/4]*/,
                           const float* b, float* out /*[n][E]*/, int E, hipStream_t st);
-hipError_t launch_add_tokens(const float* tok /*[S][C][E]*/, int S, int C, const float* posemb /*[C][E]*/,
-                             float* X /*[C][S][E] slice*/, int E, int* flag, hipStream_t st);
 // M members' decoders: X + m*xm [Q][E] -> out + m*om [Q][n_out]; scratch >= M*(Fh/64)*Q*n_out floats
 hipError_t launch_decoder(const float* X /*[Q][E]*/, int Q, const float* w1t /*[E][Fh]*/, const float* b1, int Fh,
                           const float* w2, const float* b2, int n_out, float* out, int E, hipStream_t st, int M,
                           int64_t xm, int64_t om, float* scratch);
 
+// the 16-bit modes' decoder on MFMA: X fp32 (bf16 operands) or fp16 (x_f16, fp16 operands); W1 [Fh][E] and W2p
+// [16][Fh] (pack_mlp2_perm order, rows >= n_out zero) in the operand type; Fh % 128 == 0, n_out <= 16
+hipError_t launch_decoder_mfma(const void* X, bool x_f16, int Q, const void* W1, const float* b1, int Fh, const void* W2p,
+                               const float* b2, int n_out, float* out, int E, hipStream_t st, int M, int64_t xm,
+                               int64_t om);
 // PREC_F16 state conversions: nb blocks of per_block elements (per_block % 4 == 0) at the given block
 // strides (elements); the state [T][S][E] fp16 -> the reference order [S][T][E] fp32
 hipError_t launch_f32_to_f16(const float* in, int64_t in_bstride, void* out, int64_t out_bstride, int64_t per_block,
@@ -248,7 +258,17 @@ hipError_t launch_aggregate(const float* logits /*[M][Q][n_out]*/, int M, int Q,
 hipError_t launch_layernorm_rows(const float* in, int64_t rows, int dim, float eps, void* out, bool out_f32,
                                  const float* gamma, const float* beta, hipStream_t st);
 hipError_t launch_cap_attention(const float* qp /*[cap][E]*/, const void* kv /*[S][M][2E]*/, bool kv_f32,
-                                float* out /*[S][cap][E]*/, int S, int M, int cap, int E, hipStream_t st);
+                                void* out /*[S][cap][E] fp32, or bf16 (out_bf16)*/, bool out_bf16, int S, int M, int cap,
+                                int E, hipStream_t st);
+// CAP core on MFMA (bf16; head dim 8, 24 heads = cap queries, M % 32 == 0, M <= 128): K [S*M][E], V^T [S][E][M]
+// bf16 (launch_rowgemm_ln_store's transposed form), O bf16 [S][cap][E]; hipErrorNotSupported for other shapes
+hipError_t launch_cap_attention_mfma(const float* qp, const void* K, const void* VT, void* out, int S, int M, int cap,
+                                     int E, hipStream_t st);
+// CAP tail (mlp_rows.hip, E = 192): out = LN(o2) g + b + FFN(o2), o2 = O Wout^T + bo, over M pooled tokens; O bf16,
+// Wout [E][E] bf16, W1perm / W2perm the FFN in mlp_rows order (pack_mlp1_perm / pack_mlp2_perm), vecs = [bo | b0 | g |
+// b + b3] fp32 (5E floats)
+hipError_t launch_cap_tail(const void* O, const void* Wout, const void* W1perm, const void* W2perm, const float* vecs,
+                           float* out, int64_t M, int E, float eps, hipStream_t st);
 hipError_t launch_ln_add(const float* o, const float* f, const float* g, const float* b, float* out,
                          int64_t rows, int E, float eps, hipStream_t st);
 hipError_t launch_gate_softmax(const float* x /*[S][D]*/, int64_t ldx, int S, int D, const float* w /*[n][D]*/,

@@ -100,9 +100,9 @@ __device__ __forceinline__ void cap_row(const TK* r, float (&o)[HD]) {
   }
 }
 
-template <typename TK, int HD>
+template <typename TK, typename TO, int HD>
 __global__ __launch_bounds__(1024) void cap_attn_kernel(const float* __restrict__ qp, const TK* __restrict__ kv,
-                                                        float* __restrict__ out, int M, int cap, int E, int kcmax) {
+                                                        TO* __restrict__ out, int M, int cap, int E, int kcmax) {
   extern __shared__ __attribute__((aligned(16))) unsigned char cap_lds[];
   TK* ks = (TK*)cap_lds;  // [kcmax][2E] in the storage type (bf16: 49 KB at M = 64, E = 192)
   const int s = blockIdx.x;
@@ -172,10 +172,112 @@ __global__ __launch_bounds__(1024) void cap_attn_kernel(const float* __restrict_
     }
     if (active) {
       const float inv = 1.0f / l;
-      float* o = out + ((int64_t)s * cap + c) * E + h * HD;
+      TO* o = out + ((int64_t)s * cap + c) * E + h * HD;
 #pragma unroll
-      for (int i = 0; i < HD; ++i) o[i] = acc[i] * inv;
+      for (int i = 0; i < HD; ++i) o[i] = (TO)(acc[i] * inv);
     }
+  }
+}
+
+// CAP core on MFMA (bf16 mode: head dim 8, 24 heads = 24 learned queries, M = 32 MB MGM tokens): one wave
+// per table row s, four rows per block, operands straight from HBM / L2 (no LDS):
+//   * S^T_h = K_h Q_h^T on v_mfma_f32_32x32x16_bf16, one K step = the 16 dims of a head pair: the A operand
+//     (K rows of a 32-key block, row index bits 2 and 3 swapped) serves both heads, the B operand (the
+//     constant Q^T, log2(e)/sqrt(8) folded in) is zero outside head h's 8 dims (lane half hh != h & 1);
+//   * softmax over the M keys of each query (lane = query: 16 keys per key block here, 16 in lane l ^ 32),
+//     P normalised before the product;
+//   * O^T_g += V^T_g P_h^T for the 32-dim block g = h / 4: V^T rows outside head h's 8 dims are zeroed, the
+//     P^T fragment is the S^T accumulator itself (the row swap makes a lane's 8 values 8 consecutive keys).
+// Queries >= cap (lanes r >= 24) compute garbage and are not stored.  Versus one thread per (head, query)
+// with the row's K|V staged in LDS (cap_attn_kernel): 16x the MFMA arithmetic of the real work, but no
+// scalar dot products.
+constexpr int CAPM_NH = 24;  // heads (= cap queries) of the MFMA form, head dim 8: E = 192
+template <int MB>
+__global__ __launch_bounds__(256) void cap_attn_mfma_kernel(const float* __restrict__ qp, const bf16* __restrict__ K,
+                                                            const bf16* __restrict__ VT, bf16* __restrict__ out, int S,
+                                                            int cap) {
+  constexpr int E = 8 * CAPM_NH, M = 32 * MB;
+  const int lane = threadIdx.x & 63, s = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= S) return;  // wave-uniform; no barriers below
+  const int r = lane & 31, hh = lane >> 5;
+  const float sc = kLog2e * 0.35355339059327373f;  // log2(e) / sqrt(8)
+  const bf16x8 zero8 = {};
+  const int pk = (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1);  // key of A row r (bits 2 and 3 swapped)
+  const bf16* Ks = K + (int64_t)s * M * E + (int64_t)pk * E + 8 * hh;
+  const bf16* Vs = VT + (int64_t)s * E * M + (int64_t)r * M + 8 * hh;
+  bf16* orow = out + ((int64_t)s * cap + r) * E + 4 * hh;
+#pragma unroll 1  // (six unrolled copies: 24 head bodies, beyond the instruction cache)
+  for (int g = 0; g < E / 32; ++g) {
+    bf16x8 vf[MB][2];  // V^T block g: dims 32 g + r, keys 32 kb + 16 t + 8 hh .. +7
+#pragma unroll
+    for (int kb = 0; kb < MB; ++kb)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) vf[kb][t] = *(const bf16x8*)(Vs + (int64_t)32 * g * M + 32 * kb + 16 * t);
+    f32x16 o = {};
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {  // the two head pairs of block g
+      const int p = 2 * g + pp;
+      // Q^T fragment of the pair: lane (query r, half hh) <- Q[r][16 p + 8 hh .. +7] * log2(e)/sqrt(8) (0: r >= cap)
+      bf16x8 qf;
+      {
+        const float* qr = qp + (r < cap ? r : 0) * E + 16 * p + 8 * hh;
+        const f32x4 a = *(const f32x4*)qr, b = *(const f32x4*)(qr + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qf[j] = (bf16)(r < cap ? a[j] * sc : 0.f), qf[4 + j] = (bf16)(r < cap ? b[j] * sc : 0.f);
+      }
+      bf16x8 kf[MB];
+#pragma unroll
+      for (int kb = 0; kb < MB; ++kb) kf[kb] = *(const bf16x8*)(Ks + (int64_t)32 * kb * E + 16 * p);
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        const int hq = 2 * pp + hs;  // head 4 g + hq
+        const bf16x8 qm = hh == hs ? qf : zero8;
+        f32x16 sa[MB];
+#pragma unroll
+        for (int kb = 0; kb < MB; ++kb) sa[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb], qm, f32x16{}, 0, 0, 0);
+        float m = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < MB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) m = fmaxf(m, sa[kb][i]);
+        {
+          const auto w = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+          m = fmaxf(__uint_as_float(w[0]), __uint_as_float(w[1]));
+        }
+        float l = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < MB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            sa[kb][i] = __builtin_amdgcn_exp2f(sa[kb][i] - m);
+            l += sa[kb][i];
+          }
+        {
+          const auto w = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+          l = __uint_as_float(w[0]) + __uint_as_float(w[1]);
+        }
+        const float inv = 1.0f / l;
+        const bool mine = (r >> 3) == hq;  // V^T row r of block g belongs to head 4 g + hq
+#pragma unroll
+        for (int kb = 0; kb < MB; ++kb)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            bf16x8 pf;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pf[j] = (bf16)(sa[kb][8 * t + j] * inv);
+            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(mine ? vf[kb][t] : zero8, pf, o, 0, 0, 0);
+          }
+      }
+    }
+    // O^T block g: lane (query r, half hh), element i = dim 32 g + (i & 3) + 8 (i >> 2) + 4 hh
+    if (r < cap)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        bf16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = (bf16)o[4 * k + i];
+        *(bf16x4*)(orow + 32 * g + 8 * k) = v;
+      }
   }
 }
 
@@ -256,8 +358,8 @@ hipError_t launch_layernorm_rows(const float* in, int64_t rows, int dim, float e
   return hipGetLastError();
 }
 
-template <typename TK>
-hipError_t launch_cap_t(const float* qp, const TK* kv, float* out, int S, int M, int cap, int E, hipStream_t st) {
+template <typename TK, typename TO>
+hipError_t launch_cap_t(const float* qp, const TK* kv, TO* out, int S, int M, int cap, int E, hipStream_t st) {
   // the row's keys staged in their storage type, chunks of up to 64 keys within 96 KiB of LDS
   if (E % 4 != 0) return hipErrorInvalidValue;
   const int kcmax = max(1, min(CAP_STAGE, 98304 / (2 * E * (int)sizeof(TK))));
@@ -265,28 +367,46 @@ hipError_t launch_cap_t(const float* qp, const TK* kv, float* out, int S, int M,
   const int pairs = cap * cap;
   dim3 g(S), b((unsigned)min(1024, (pairs + 63) / 64 * 64));
   switch (E / cap) {
-    case 96: hipLaunchKernelGGL((cap_attn_kernel<TK, 96>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
-    case 48: hipLaunchKernelGGL((cap_attn_kernel<TK, 48>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
-    case 24: hipLaunchKernelGGL((cap_attn_kernel<TK, 24>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
-    case 16: hipLaunchKernelGGL((cap_attn_kernel<TK, 16>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
-    case 12: hipLaunchKernelGGL((cap_attn_kernel<TK, 12>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
-    case 8: hipLaunchKernelGGL((cap_attn_kernel<TK, 8>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
-    case 6: hipLaunchKernelGGL((cap_attn_kernel<TK, 6>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
-    case 4: hipLaunchKernelGGL((cap_attn_kernel<TK, 4>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
-    case 3: hipLaunchKernelGGL((cap_attn_kernel<TK, 3>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
-    case 2: hipLaunchKernelGGL((cap_attn_kernel<TK, 2>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
-    case 1: hipLaunchKernelGGL((cap_attn_kernel<TK, 1>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 96: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 96>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 48: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 48>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 24: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 24>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 16: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 16>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 12: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 12>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 8: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 8>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 6: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 6>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 4: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 4>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 3: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 3>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 2: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 2>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
+    case 1: hipLaunchKernelGGL((cap_attn_kernel<TK, TO, 1>), g, b, lds, st, qp, kv, out, M, cap, E, kcmax); break;
     default: return hipErrorInvalidValue;  // cap_heads with E / cap outside the instantiated set
   }
   return hipGetLastError();
 }
 
-hipError_t launch_cap_attention(const float* qp, const void* kv, bool kv_f32, float* out, int S, int M, int cap, int E,
-                                hipStream_t st) {
+hipError_t launch_cap_attention(const float* qp, const void* kv, bool kv_f32, void* out, bool out_bf16, int S, int M,
+                                int cap, int E, hipStream_t st) {
   if (S <= 0) return hipSuccess;
   if (E % cap != 0) return hipErrorInvalidValue;
-  if (kv_f32) return launch_cap_t(qp, (const float*)kv, out, S, M, cap, E, st);
-  return launch_cap_t(qp, (const bf16*)kv, out, S, M, cap, E, st);
+  if (kv_f32) return out_bf16 ? launch_cap_t(qp, (const float*)kv, (bf16*)out, S, M, cap, E, st)
+                              : launch_cap_t(qp, (const float*)kv, (float*)out, S, M, cap, E, st);
+  return out_bf16 ? launch_cap_t(qp, (const bf16*)kv, (bf16*)out, S, M, cap, E, st)
+                  : launch_cap_t(qp, (const bf16*)kv, (float*)out, S, M, cap, E, st);
+}
+
+hipError_t launch_cap_attention_mfma(const float* qp, const void* K, const void* VT, void* out, int S, int M, int cap,
+                                     int E, hipStream_t st) {
+  if (S <= 0) return hipSuccess;
+  if (E != 8 * CAPM_NH || cap != CAPM_NH || M % 32 != 0 || M > 128 || M <= 0) return hipErrorNotSupported;
+  const dim3 grid((unsigned)((S + 3) / 4));
+  const bf16 *k = (const bf16*)K, *vt = (const bf16*)VT;
+  bf16* o = (bf16*)out;
+  switch (M / 32) {
+    case 1: hipLaunchKernelGGL((cap_attn_mfma_kernel<1>), grid, dim3(256), 0, st, qp, k, vt, o, S, cap); break;
+    case 2: hipLaunchKernelGGL((cap_attn_mfma_kernel<2>), grid, dim3(256), 0, st, qp, k, vt, o, S, cap); break;
+    case 3: hipLaunchKernelGGL((cap_attn_mfma_kernel<3>), grid, dim3(256), 0, st, qp, k, vt, o, S, cap); break;
+    default: hipLaunchKernelGGL((cap_attn_mfma_kernel<4>), grid, dim3(256), 0, st, qp, k, vt, o, S, cap); break;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_ln_add(const float* o, const float* f, const float* g, const float* b, float* out, int64_t rows,

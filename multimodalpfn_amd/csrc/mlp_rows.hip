@@ -69,12 +69,19 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
 // but measured 15% slower: one wave cannot hide the LDS / GELU latency the second wave covers)
 // NW = waves per block: 4 (two blocks per CU, each DMA-filling its own rings) or 8 (one block per CU:
 // each weight byte crosses into LDS once per CU; waves 0-3 fill the W1 ring, 4-7 the W2 ring)
-template <int TT, bool RES, int NW, bool F16>
+// CAP (with RES, bf16): the CrossAttentionPooler's tail (transformer.py:85-86) on its pooled tokens:
+//   o2 = O Wout^T + bo;  X <- LayerNorm(o2) g + b + (GELU(o2 W1^T + b0) W2^T + b3)
+// (the prologue's residual is the bias, its LayerNorm moves to the end beside the FFN, exact-erf GELU);
+// the vectors [bo | b0 | g | b + b3] sit in LDS beside the rings (capb, CAPL floats).
+constexpr int CAPL = 5 * RE;  // bo, b0 (2 RE), g, b + b3
+template <int TT, bool RES, int NW, bool F16, bool CAP = false>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_rows_kernel(void* __restrict__ Xv,
                                                                        const void* __restrict__ W1v,
                                                                        const void* __restrict__ W2v, int M, int Fh,
                                                                        float eps, const void* __restrict__ Ov,
-                                                                       const void* __restrict__ Woutv) {
+                                                                       const void* __restrict__ Woutv,
+                                                                       const float* __restrict__ capb) {
+  static_assert(!CAP || (RES && !F16), "the CAP tail runs the bf16 prologue form");
   typedef typename Op16<F16>::t HT;  // operand element
   typedef typename Op16<F16>::x8 X8;
   typedef __attribute__((ext_vector_type(2))) HT HT2;
@@ -86,7 +93,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
   const HT* __restrict__ Wout = (const HT*)Woutv;
   constexpr int RROWS = NW * 16 * TT;  // rows per block
   __shared__ __attribute__((aligned(1024))) bf16 lds[LDS_B / 2];
+  __shared__ __attribute__((aligned(16))) float capl[CAP ? CAPL : 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if constexpr (CAP)  // before any LDS-DMA: the compiler's own vmcnt waits cover these loads alone
+    for (int i = tid; i < CAPL; i += 64 * NW) capl[i] = capb[i];
   const int wg = wave & 3;                           // the wave's share of a ring fill
   const bool gw1 = NW == 4 || wave < 4, gw2 = NW == 4 || wave >= 4;  // fills W1 / W2 pieces
   const int fr = lane & 15, fg = lane >> 4;
@@ -192,7 +202,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
       }
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        if (hf == 1) load_x();  // (program order: half 0, O, X, half 1 -- see the waits below)
+        if (hf == 1 && !CAP) load_x();  // (program order: half 0, O, X, half 1 -- see the waits below)
         if (NW == 4 || (wave >> 2) == hf)  // NW 8: waves 0-3 half 0, 4-7 half 1
 #pragma unroll
           for (int j = 0; j < 9; ++j)
@@ -227,6 +237,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     };
     wait_vm(integral_constant<int, 9>{});  // half 0 (and O, X) landed; half 1 may fly
     __syncthreads();
+    if constexpr (CAP)  // the out-projection accumulates onto its bias
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+        for (int f = 0; f < RE / 16; ++f) y[f][tt] = *(const f32x4*)(capl + f * 16 + fg * 4);
     outproj(integral_constant<int, 0>{});
     __syncthreads();  // every wave is done with half 0: the W1 ring is free
     dma_w1(0, 0);
@@ -241,6 +256,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     dma_w2(0, 0);
     if (nchunks > 1) dma_w2(1, 1);
     // residual (already in y) + LayerNorm (layer.py:437-455), packed as the MLP's A^T fragments
+    float mu[TT], iv[TT];
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
       float sm = 0.f;
@@ -257,12 +273,28 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
           const float dl = y[f][tt][i] - mean;
           q += dl * dl;
         }
-      const float inv = 1.0f / sqrtf(sum_rows4(q) * (1.0f / RE) + eps);
+      mu[tt] = mean, iv[tt] = 1.0f / sqrtf(sum_rows4(q) * (1.0f / RE) + eps);
+      if constexpr (CAP) {
+        to_af(tt);  // the FFN reads o2 itself
+      } else {
 #pragma unroll
-      for (int f = 0; f < RE / 16; ++f)
+        for (int f = 0; f < RE / 16; ++f)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) y[f][tt][i] = (y[f][tt][i] - mean) * inv;
-      to_af(tt);
+          for (int i = 0; i < 4; ++i) y[f][tt][i] = (y[f][tt][i] - mean) * iv[tt];
+        to_af(tt);
+      }
+    }
+    if constexpr (CAP) {  // y restarts as out_norm(o2) + b3: one tile's g / (b + b3) live at a time
+#pragma unroll
+      for (int f = 0; f < RE / 16; ++f) {
+        asm volatile("" ::: "memory");  // (g / b loads hoisted above the LayerNorm spilled ~110 VGPRs)
+        const int e = f * 16 + fg * 4;
+        const f32x4 g = *(const f32x4*)(capl + 3 * RE + e), bb = *(const f32x4*)(capl + 4 * RE + e);
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) y[f][tt][i] = fmaf((y[f][tt][i] - mu[tt]) * iv[tt], g[i], bb[i]);
+      }
     }
     // before H(0): W1(0) landed (newer: W1(1), W1(2), W2(0), W2(1); NW 8: each group its own two)
     if (deep) wait_vm(integral_constant<int, (NW == 8 ? 2 : 4) * MP>{});
@@ -284,16 +316,22 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
 
   // GELU of one adjacent pair q (0 .. 4 TT - 1: tile tt, half ht, elements 2 (q & 1) + 0, 1) of a chunk's
   // H^T accumulators, packed into its bf16 B fragment for the down-projection
-  auto gelu_pair = [&](auto qc, const f32x4 (&hs)[2][TT], X8 (&hb)[TT]) {
+  auto gelu_pair = [&](auto qc, const f32x4 (&hs)[2][TT], X8 (&hb)[TT], int c) {
     constexpr int q = decltype(qc)::value, tt = q >> 2, ht = (q >> 1) & 1, i = 2 * (q & 1);
-    const HT2 pr =
-        __builtin_convertvector((float2_t){gelu_tanh_fast(hs[ht][tt][i]), gelu_tanh_fast(hs[ht][tt][i + 1])}, HT2);
+    HT2 pr;
+    if constexpr (CAP) {  // hidden bias b0 (hidden c*32 + 16 ht + 4 fg + i of the H^T tile), exact GELU
+      const float2_t bb = *(const float2_t*)(capl + RE + c * RHC + 16 * ht + 4 * fg + i);
+      pr = __builtin_convertvector((float2_t){gelu_erf(hs[ht][tt][i] + bb[0]), gelu_erf(hs[ht][tt][i + 1] + bb[1])},
+                                   HT2);
+    } else {
+      pr = __builtin_convertvector((float2_t){gelu_tanh_fast(hs[ht][tt][i]), gelu_tanh_fast(hs[ht][tt][i + 1])}, HT2);
+    }
     hb[tt][4 * ht + i] = pr[0];
     hb[tt][4 * ht + i + 1] = pr[1];
   };
   // H^T [32 hidden][16 TT rows] = W1c . A^T  (W1c in W1 slot SL); with G, the previous chunk's GELU
   // (hs -> hb) rides in the k-steps' MFMA shadows (pairs 0..4TT-1 spread over the RE/32 k-steps)
-  auto hmma = [&](auto slc, f32x4 (&h)[2][TT], auto gc, const f32x4 (&hs)[2][TT], X8 (&hb)[TT]) {
+  auto hmma = [&](auto slc, f32x4 (&h)[2][TT], auto gc, const f32x4 (&hs)[2][TT], X8 (&hb)[TT], int c) {
     constexpr bool G = decltype(gc)::value;
     constexpr int SL = decltype(slc)::value;
     auto w1frag = [&](int ht, int ks) {
@@ -326,7 +364,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
         constexpr int NPQ = 4 * TT, NKS = RE / 32;
         static_for<NPQ>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
-          if (q * NKS / NPQ == ks) gelu_pair(qc, hs, hb);
+          if (q * NKS / NPQ == ks) gelu_pair(qc, hs, hb, c);
         });
       }
     }
@@ -336,7 +374,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
   f32x4 h[2][TT];
   {
     X8 unused[TT];
-    hmma(S0{}, h, std::false_type{}, h, unused);
+    hmma(S0{}, h, std::false_type{}, h, unused, 0);
   }
   // before chunk 0: W1(1) and W2(0) landed (only W2(1) may fly); the barrier also keeps chunk 0 from
   // refilling W1 slot 0 (with W1(3)) while a lagging wave still reads W1(0) above
@@ -359,7 +397,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     X8 hb[TT];
     {
       f32x4 hn[2][TT];
-      hmma(std::integral_constant<int, (PAR + 1) % 3>{}, hn, std::true_type{}, h, hb);
+      hmma(std::integral_constant<int, (PAR + 1) % 3>{}, hn, std::true_type{}, h, hb, c);
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
@@ -410,6 +448,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     const int64_t m = m0 + tt * 16 + fr;
     const bool valid = m < M;
     float* xr = X + (valid ? m : (int64_t)M - 1) * RE + fg * 4;
+    if constexpr (CAP) {  // out_norm(o2) + b3 + FFN: no LayerNorm after the sum
+      if (valid)
+#pragma unroll
+        for (int o = 0; o < RE / 16; ++o) *(f32x4*)(xr + o * 16) = y[o][tt];
+      continue;
+    }
     float s = 0.f;
 #pragma unroll
     for (int o = 0; o < RE / 16; ++o)
@@ -459,6 +503,16 @@ hipError_t launch_mr(void* X, const void* W1, const void* W2, int64_t M, int Fh,
                      const void* O, const void* Wout);
 }  // namespace
 
+hipError_t launch_cap_tail(const void* O, const void* Wout, const void* W1perm, const void* W2perm, const float* vecs,
+                           float* out, int64_t M, int E, float eps, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (E != RE || !O || !Wout || !W1perm || !W2perm || !vecs || !out) return hipErrorInvalidValue;
+  constexpr int RROWS = 16 * 4 * 2;
+  hipLaunchKernelGGL((mlp_rows_kernel<2, true, 4, false, true>), dim3((unsigned)((M + RROWS - 1) / RROWS)), dim3(256),
+                     0, st, (void*)out, W1perm, W2perm, (int)M, 2 * RE, eps, O, Wout, vecs);
+  return hipGetLastError();
+}
+
 hipError_t launch_mlp_rows(void* X, const void* W1perm, const void* W2perm, int64_t M, int E, int Fh, float eps,
                            hipStream_t st, const void* O, const void* Wout, bool f16) {
   if (M <= 0) return hipSuccess;
@@ -481,10 +535,10 @@ hipError_t launch_mr(void* X, const void* W1perm, const void* W2perm, int64_t M,
   const dim3 grid((unsigned)((M + RROWS - 1) / RROWS)), block(64 * MLP_NW);
   if (O)
     hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, true, MLP_NW, F16>), grid, block, 0, st, X, W1perm, W2perm, (int)M,
-                       Fh, eps, O, Wout);
+                       Fh, eps, O, Wout, nullptr);
   else
     hipLaunchKernelGGL((mlp_rows_kernel<MLP_TT, false, MLP_NW, F16>), grid, block, 0, st, X, W1perm, W2perm, (int)M,
-                       Fh, eps, nullptr, nullptr);
+                       Fh, eps, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 }  // namespace

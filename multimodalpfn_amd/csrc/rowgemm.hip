@@ -318,10 +318,13 @@ __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p, in
 // (N % 64 == 0): the CAP K|V projection of the normalised mixer tokens (transformer.py:77-84) in
 // one pass -- the LayerNorm (no affine; folded into W on the host) runs on the rows in registers,
 // so the normalised copy never reaches HBM.  Same chunk pipeline and LDS-staged 16-B stores as
-// the QKV kernel above.
+// the QKV kernel above.  vt_from >= 0: outputs [vt_from, N) go transposed per group of Mk rows
+// (Mk % 32 == 0), CT [M / Mk][N - vt_from][Mk] (the CAP V^T: keys contiguous), the rest to C with
+// row stride ldc.
 __global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const float* __restrict__ A, const bf16* __restrict__ W,
                                                                   const float* __restrict__ bias, bf16* __restrict__ C,
-                                                                  int M, int N, float eps, int do_ln) {
+                                                                  int M, int N, float eps, int do_ln, int ldc,
+                                                                  bf16* __restrict__ CT, int vt_from, int Mk) {
   __shared__ __attribute__((aligned(16))) uint16_t Ws[2 * QCEL + 4 * OWEL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
@@ -391,6 +394,33 @@ __global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const float* _
     f32x4 acc[QC / 16][2];
 #pragma unroll
     for (int f = 0; f < QC / 16; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (vt_from >= 0 && c * QC >= vt_from) {  // block-uniform
+      chunk_mma<false>(Wc, af, fr, fg, acc);
+      // C: lane = feature 16f + fr, rows 16tt + 4fg + i  ->  Os[feature][row] (+ bias)
+#pragma unroll
+      for (int f = 0; f < QC / 16; ++f) {
+        const float bv = bias[c * QC + f * 16 + fr];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          bf16x4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = (bf16)(acc[f][tt][i] + bv);
+          *(bf16x4*)(Os + (f * 16 + fr) * OVST + tt * 16 + fg * 4) = o;
+        }
+      }
+      if (m0 < M) {  // the wave's 32 rows are keys j0 .. j0 + 31 of group g0 (Mk % 32 == 0, M % Mk == 0)
+        const int64_t g0 = m0 / Mk;
+        const int j0 = (int)(m0 - g0 * Mk), nv = N - vt_from;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int feat = 16 * i + (lane >> 2), rr = (lane & 3) * 8;
+          const u32x4 v = *(const u32x4*)(Os + feat * OVST + rr);
+          *(u32x4*)(CT + (g0 * nv + c * QC - vt_from + feat) * Mk + j0 + rr) = v;
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     chunk_mma<true>(Wc, af, fr, fg, acc);
     // C^T: lane = row 16tt + fr, features 16f + 4fg + i  ->  Os[row][feature] (+ bias)
 #pragma unroll
@@ -408,7 +438,7 @@ __global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const float* _
     for (int i = 0; i < 4; ++i) {  // 32 rows x 8 chunks of 16 B
       const int row = 8 * i + (lane >> 3), cc = lane & 7;
       const u32x4 v = *(const u32x4*)(Os + row * OQST + cc * 8);
-      if (m0 + row < M) *(u32x4*)(C + (m0 + row) * N + c * QC + cc * 8) = v;  // (C: bf16 elements)
+      if (m0 + row < M) *(u32x4*)(C + (m0 + row) * ldc + c * QC + cc * 8) = v;  // (C: bf16 elements)
     }
     __syncthreads();
   }
@@ -556,11 +586,15 @@ hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, void* X
 }
 
 hipError_t launch_rowgemm_ln_store(const float* A, const void* W, const float* bias, void* C, int64_t M, int N,
-                                   float eps, bool ln, hipStream_t st) {
+                                   float eps, bool ln, hipStream_t st, void* CT, int vt_from, int Mk) {
   if (M <= 0) return hipSuccess;
   if (N % QC != 0 || N <= 0 || M > INT32_MAX) return hipErrorInvalidValue;
+  if (CT && (vt_from < 0 || vt_from % QC != 0 || vt_from >= N || Mk <= 0 || Mk % 32 != 0 || M % Mk != 0))
+    return hipErrorInvalidValue;
+  const int ldc = CT ? vt_from : N;
   hipLaunchKernelGGL(rowgemm_ln_store_kernel, dim3((unsigned)((M + GROWS - 1) / GROWS)), dim3(256), 0, st, A,
-                     (const bf16*)W, bias, (bf16*)C, (int)M, N, eps, ln ? 1 : 0);
+                     (const bf16*)W, bias, (bf16*)C, (int)M, N, eps, ln ? 1 : 0, ldc, (bf16*)CT, CT ? vt_from : -1,
+                     CT ? Mk : 1);
   return hipGetLastError();
 }
 

@@ -100,8 +100,10 @@ def test_fp8_attention_tile_bodies(variant, cvt):
 
 @pytest.mark.parametrize("src,needle,limit", [
     ("attention_pipe.hip", "attn_pipe_kernel", 0),
-    ("mlp_rows.hip", "mlp_rows_kernelILi2ELb1E", 0),
+    ("mlp_rows.hip", "mlp_rows_kernelILi2ELb1ELi4ELb0ELb0E", 0),
+    ("mlp_rows.hip", "mlp_rows_kernelILi2ELb1ELi4ELb1ELb0E", 0),
     ("mlp_rows.hip", "mlp_rows_kernelILi2ELb0E", 0),
+    ("mlp_rows.hip", "mlp_rows_kernelILi2ELb1ELi4ELb0ELb1E", 96),  # CAP tail: one-time prologue spills
     ("rowgemm.hip", "rowgemm_qkv2_kernel", 0),
     ("featrow.hip", "feat_rows_kernelILi3ELb0E", 48),  # one-time spills outside the head loop
     ("featrow.hip", "feat_rows_kernelILi3ELb1E", 56),  # PREC_F16: X^T fragments live to the residual
@@ -120,7 +122,7 @@ def test_mlp_gelu_rides_in_the_up_projection(variant, mm):
     block, whose MFMAs consume it.  Now each chunk is one block (up-projection of the next
     chunk + this chunk's GELU + down-projection, 48 MFMAs, 16 exps); only the pre-loop up-projection of
     chunk 0 (24 MFMAs) has no GELU to carry."""
-    body = _function(_asm("mlp_rows.hip"), f"mlp_rows_kernelILi2ELb1ELi4E{variant}")
+    body = _function(_asm("mlp_rows.hip"), f"mlp_rows_kernelILi2ELb1ELi4E{variant}Lb0E")
     blocks = [c for c in _blocks(body) if 24 <= c[mm] < 72]
     bare = [c for c in blocks if c["v_exp_f32_e32"] == 0]
     chunks = [c for c in blocks if c[mm] == 48 and c["v_exp_f32_e32"] == 16]
@@ -165,5 +167,6 @@ def test_hot_kernels_use_no_scratch(src, extra):
     asm = _asm(src, extra)
     sizes = re.findall(r"\.name:\s+(\S+)\n(?:.*\n)*?\s+\.private_segment_fixed_size: (\d+)", asm)
     assert sizes
-    bad = [(n, int(v)) for n, v in sizes if int(v)]
+    # the CAP tail (mixer, once per predict) spills row addresses once in its prologue (tests the limit above)
+    bad = [(n, int(v)) for n, v in sizes if int(v) and "mlp_rows_kernelILi2ELb1ELi4ELb0ELb1E" not in n]
     assert not bad, bad

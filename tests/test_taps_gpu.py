@@ -105,6 +105,37 @@ def test_taps_at_config_c_shape(prec):
             assert err <= (TOL[prec] if prec in (1, 5) else 1e-4), (name, err)
 
 
+@pytest.mark.parametrize("prec", [1, 0])
+@pytest.mark.parametrize("n_mod,S", [(1, 301), (2, 97), (1, 1)])
+def test_mixer_taps_at_config_c_shape(n_mod, S, prec):
+    """MGM 64 + CAP 24 (the config C / D mixer: M = 64 / 128 MGM tokens per row) against the oracle in fp32 on
+    the GPU.  In the bf16 mode this shape takes the MFMA CAP attention (K and V^T from the projection, one wave
+    per row, S % 4 != 0 leaves a block's waves idle) and the row-resident CAP tail (mlp_rows CAP form)."""
+    from synth import synth_state_dict
+
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    torch.backends.cuda.matmul.allow_tf32 = False
+    cfg = ModelConfig(nlayers=1, mgm_heads=64, cap_heads=24)
+    sd = synth_state_dict(state_dict_spec(cfg), 4)
+    eng = _engine(cfg, sd)
+    spec, w = oracle_spec(cfg), {k: v.cuda() for k, v in torch_sd(sd).items()}
+    g = torch.Generator(device="cpu").manual_seed(5 + n_mod)
+    im = torch.randn(S, n_mod, 768, generator=g).cuda()
+    with torch.inference_mode():
+        ref = oracle_mgm(spec, w, im)
+        got = eng.mgm(im, prec)
+        err = rel_err(got.cpu().numpy(), ref.cpu().numpy())
+        print(f"mgm n_mod {n_mod} prec {prec}: rel err {err:.2e}")
+        assert err <= (TOL[prec] if prec == 1 else 1e-4), err
+        ref_c = oracle_cap(spec, w, ref)
+        got_c = eng.cap(ref, prec)
+        assert got_c.shape == ref_c.shape and torch.isfinite(got_c).all()
+        err = rel_err(got_c.cpu().numpy(), ref_c.cpu().numpy())
+        print(f"cap n_mod {n_mod} prec {prec}: rel err {err:.2e}")
+        assert err <= (TOL[prec] if prec == 1 else 1e-4), err
+
+
 @pytest.mark.parametrize("prec", [1, 0, 5])
 @pytest.mark.parametrize("S,T", [(1, 1), (5, 16), (130, 17), (7, 33), (66, 48), (3, 49), (129, 64), (9, 65)])
 def test_taps_ragged_shapes(S, T, prec):
