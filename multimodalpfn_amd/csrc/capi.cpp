@@ -308,7 +308,7 @@ int finalize(mmpfn_ctx* ctx) {
     if ((rc = upload(ctx, ctx->dec_b1, *db1, false))) return rc;
     if ((rc = upload(ctx, ctx->dec_w2, *dw2, false))) return rc;
     if ((rc = upload(ctx, ctx->dec_b2, *db2, false))) return rc;
-    if (d.n_out <= 16 && Fh % 128 == 0 && E % 32 == 0) {
+    if (d.n_out <= 16 && Fh % 128 == 0 && E % 32 == 0 && E <= 256) {
       std::vector<float> w2p((size_t)16 * Fh, 0.f);
       std::copy(dw2->begin(), dw2->end(), w2p.begin());
       w2p = pack_mlp2_perm(w2p, 16, Fh);

@@ -460,23 +460,33 @@ __global__ __launch_bounds__(256) void dec_mfma_kernel(const TX* __restrict__ X,
   const TX* xr = X + m * xm + (int64_t)min(q0 + fr, Q - 1) * E + 8 * fg;
   const int hw = Fh / 4, h0 = wave * hw;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};  // out^T tile: lane (row fr, outputs 4 fg + i)
-  for (int hc = 0; hc < hw; hc += 32) {  // 32 hidden units: tiles t = 0, 1
-    f32x4 h[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    for (int ks = 0; ks < E / 32; ++ks) {
-      X8 xb;
+  X8 xb[8];  // the rows' X fragments, every k-step (E <= 256), loaded once
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    if (ks < E / 32) {
       if constexpr (F16) {
-        xb = *(const X8*)(xr + 32 * ks);
+        xb[ks] = *(const X8*)(xr + 32 * ks);
       } else {
         const f32x4 a = *(const f32x4*)(xr + 32 * ks), b = *(const f32x4*)(xr + 32 * ks + 4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xb[j] = (HT)a[j], xb[4 + j] = (HT)b[j];
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const X8 wa = *(const X8*)(W1 + (int64_t)(h0 + hc + 16 * t + fr) * E + 32 * ks + 8 * fg);
-        h[t] = mfma16x(wa, xb, h[t]);
+        for (int j = 0; j < 4; ++j) xb[ks][j] = (HT)a[j], xb[ks][4 + j] = (HT)b[j];
       }
     }
+  }
+  for (int hc = 0; hc < hw; hc += 32) {  // 32 hidden units: tiles t = 0, 1
+    X8 wa[8][2];  // the chunk's W1 fragments, all issued before its MFMAs
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (ks < E / 32) wa[ks][t] = *(const X8*)(W1 + (int64_t)(h0 + hc + 16 * t + fr) * E + 32 * ks + 8 * fg);
+    const X8 wb = *(const X8*)(W2 + (int64_t)fr * Fh + h0 + hc + 8 * fg);
+    f32x4 h[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (ks < E / 32) h[t] = mfma16x(wa[ks][t], xb[ks], h[t]);
     // G^T fragment: lane (row fr, fg) <- hidden hc + 16 (j / 4) + 4 fg + j % 4 (the pack_mlp2_perm order)
     X8 gb;
 #pragma unroll
@@ -486,7 +496,6 @@ __global__ __launch_bounds__(256) void dec_mfma_kernel(const TX* __restrict__ X,
         const int hid = h0 + hc + 16 * t + 4 * fg + i;
         gb[4 * t + i] = (HT)gelu_erf(h[t][i] + b1[hid]);
       }
-    const X8 wb = *(const X8*)(W2 + (int64_t)fr * Fh + h0 + hc + 8 * fg);
     acc = mfma16x(wb, gb, acc);
   }
   part[wave][lane] = acc;
@@ -639,7 +648,7 @@ hipError_t launch_decoder_mfma(const void* X, bool x_f16, int Q, const void* W1,
                                const float* b2, int n_out, float* out, int E, hipStream_t st, int M, int64_t xm,
                                int64_t om) {
   if (Q <= 0 || M <= 0) return hipSuccess;
-  if (E % 32 != 0 || Fh % 128 != 0 || n_out > 16 || n_out <= 0) return hipErrorInvalidValue;
+  if (E % 32 != 0 || E > 256 || Fh % 128 != 0 || n_out > 16 || n_out <= 0) return hipErrorInvalidValue;
   const dim3 grid((unsigned)((Q + 15) / 16), (unsigned)M);
   if (x_f16)
     hipLaunchKernelGGL((dec_mfma_kernel<f16>), grid, dim3(256), 0, st, (const f16*)X, Q, xm, W1, b1, Fh, W2p, b2, n_out,
