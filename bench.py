@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--attn-reps", type=int, default=20)
     p.add_argument("--lanes", type=int, default=None, help="concurrent member lanes per GPU (default: engine's)")
     p.add_argument("--batch", type=int, default=None, help="members per batched forward (default: engine's)")
+    p.add_argument("--mixer-stream", action="store_true",
+                   help="headline step: the mixer on its own stream, overlapping the previous step's forwards")
     p.add_argument("--api-steps", type=int, default=3, help="timed predict_proba calls of the API leg (0: skip)")
     p.add_argument("--no-kv-cache", dest="kv_cache", action="store_false", help="skip the fit_with_cache leg")
     p.add_argument("--no-config-d", dest="config_d", action="store_false", help="skip the config-D leg")
@@ -418,17 +420,29 @@ def timed_steps(step, steps, warmup, world, device):
     return dt
 
 
-def make_step(eng, members, mine, assignment, rank, img, prec, lanes, batch):
+def make_step(eng, members, mine, assignment, rank, img, prec, lanes, batch, mixer_stream=False):
     """One predict_proba of the hot path on device-resident inputs (classifier.py:517-576 minus the
     host-side input validation / per-member transform and the final copy to host): the mixer once,
     this rank's members through forward_many, one RCCL all-gather of the logits, the ensemble
-    softmax-mean on the device."""
+    softmax-mean on the device.  mixer_stream: the mixer runs on its own stream, ordered only after the
+    previous step's mixer (its input image is resident and never written), so the next step's modality
+    projection overlaps this step's member forwards; the step's members wait for its tokens."""
     from multimodalpfn_amd.parallel import allgather_logits
 
     perms = np.stack([m[2] for m in members])
+    mix = torch.cuda.Stream(eng.device) if mixer_stream else None
 
     def step():
-        tokens = eng.mixer_tokens(img, prec)
+        if mix is not None:
+            with torch.cuda.stream(mix):
+                tokens = eng.mixer_tokens(img, prec)
+                ev = torch.cuda.Event()
+                ev.record(mix)
+            cur = torch.cuda.current_stream(eng.device)
+            cur.wait_event(ev)
+            tokens.record_stream(cur)
+        else:
+            tokens = eng.mixer_tokens(img, prec)
         outs = eng.forward_many([(members[m][0], tokens, members[m][1]) for m in mine], prec, lanes, batch)
         allm = allgather_logits(torch.stack(outs), assignment, rank)
         return eng.aggregate(allm, perms, N_CLASSES, 0.9, False)
@@ -622,7 +636,7 @@ def main():
     T = (N_FEAT + 1) // 2 + CAP + 1
     assignment = lpt_assign([member_cost(T, S_ROWS, N_TRAIN)] * M, world, [T] * M, args.batch or eng.batch)
     mine = assignment[rank]
-    step = make_step(eng, members, mine, assignment, rank, img, prec, args.lanes, args.batch)
+    step = make_step(eng, members, mine, assignment, rank, img, prec, args.lanes, args.batch, args.mixer_stream)
 
     probs = step()
     eng.status()  # NaN check once (reference raises ValueError)

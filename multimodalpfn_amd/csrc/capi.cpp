@@ -845,7 +845,8 @@ int decode(mmpfn_ctx* ctx, float* logits, int M = 1) {
 }
 
 // MGM head bank (transformer.py:33-57): image [S][n_mod][D] -> tokens [S][mgm*n_mod][E] (head-major)
-int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* mtok, int prec) {
+// tok_bf16: the tokens in bf16 (the MGM+CAP chain's intermediate; bf16 mode, E = 192 only)
+int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, void* mtok, int prec, bool tok_bf16 = false) {
   const mmpfn_model_desc& d = ctx->d;
   const int E = d.emsize, D = d.nhid;
   const bool bf = prec == PREC_BF16;
@@ -859,6 +860,7 @@ int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* mtok,
   GemmArgs a = gargs();
   a.A = ctx->mx[0].p, a.lda = D, setw(ctx, a, ctx->mgm_w1, ctx->mgm_w1_h, prec), a.bias = (const float*)ctx->mgm_b1.p;
   a.M = (int)rows, a.N = mg * D, a.K = D, a.C = ctx->mx[1].p, a.ldc = (int64_t)mg * (D / 2);
+  const bool big2 = bf && E == 192 && (D / 2) % 32 == 0;  // the big-tile down-projection (bf16 tokens possible)
   if (bf && (mg * D) % 256 == 0 && D % 64 == 0)
     HIPCHK(launch_gemm_glu_big(ctx->mx[0].p, a.W, a.bias, ctx->mx[1].p, (int)rows, mg * D, D, st));
   else
@@ -869,12 +871,18 @@ int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* mtok,
   b.bias = (const float*)ctx->mgm_b2.p, b.b_zstride = E;
   b.M = (int)rows, b.N = E, b.K = D / 2;
   b.C = mtok, b.ldc = E, b.rdiv2 = n_mod, b.rmul2 = M, b.zmul = n_mod;
-  HIPCHK(launch_gemm(b, prec, EPI_REMAP, !bf, true, mg, st));
+  if (tok_bf16 && !big2) return fail(ctx, MMPFN_ERR_INVALID, "bf16 MGM tokens");
+  if (big2)
+    HIPCHK(launch_gemm_remap_big(ctx->mx[1].p, (int64_t)mg * (D / 2), ctx->mgm_w2_h.p, (const float*)ctx->mgm_b2.p, mtok,
+                                 tok_bf16, (int)rows, D / 2, mg, n_mod, E, st));
+  else
+    HIPCHK(launch_gemm(b, prec, EPI_REMAP, !bf, true, mg, st));
   return MMPFN_OK;
 }
 
 // CrossAttentionPooler (transformer.py:60-88): MGM tokens [S][M][E] -> tokens [S][cap][E]
-int mixer_cap(mmpfn_ctx* ctx, const float* mtok, int S, int M, float* tokens, int prec) {
+// mtok fp32, or bf16 (in_bf16: from mixer_mgm's bf16 form)
+int mixer_cap(mmpfn_ctx* ctx, const void* mtok, int S, int M, float* tokens, int prec, bool in_bf16 = false) {
   const mmpfn_model_desc& d = ctx->d;
   const int E = d.emsize;
   const bool bf = prec == PREC_BF16;
@@ -891,10 +899,10 @@ int mixer_cap(mmpfn_ctx* ctx, const float* mtok, int S, int M, float* tokens, in
   const bool mf = bf && E == 192 && cap == 24 && M % 32 == 0 && M <= 128 && ctx->cap_vecs.p;
   void* vt = (char*)ctx->mx[4].p + (size_t)srows * E * 2;
   if (bf && E == 192) {  // k_norm + K|V projection in one row pass (normalised rows stay in registers)
-    HIPCHK(launch_rowgemm_ln_store(mtok, ctx->cap_kv_h.p, (const float*)ctx->cap_kv_b.p, ctx->mx[4].p, srows, 2 * E,
-                                   1e-5f, true, st, mf ? vt : nullptr, E, M));
+    HIPCHK(launch_rowgemm_ln_store(mtok, in_bf16, ctx->cap_kv_h.p, (const float*)ctx->cap_kv_b.p, ctx->mx[4].p, srows,
+                                   2 * E, 1e-5f, true, st, mf ? vt : nullptr, E, M));
   } else {
-    HIPCHK(launch_layernorm_rows(mtok, srows, E, 1e-5f, ctx->mx[3].p, !bf, nullptr, nullptr, st));
+    HIPCHK(launch_layernorm_rows((const float*)mtok, srows, E, 1e-5f, ctx->mx[3].p, !bf, nullptr, nullptr, st));
     GemmArgs c = gargs();
     c.A = ctx->mx[3].p, c.lda = E, setw(ctx, c, ctx->cap_kv, ctx->cap_kv_h, prec), c.bias = (const float*)ctx->cap_kv_b.p;
     c.M = (int)srows, c.N = 2 * E, c.K = E, c.C = ctx->mx[4].p, c.ldc = 2 * E;
@@ -942,8 +950,9 @@ int mixer(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, i
   if (d.mixer_type == MMPFN_MIXER_MGM_CAP) {
     const int M = d.mgm_heads * n_mod;
     RC(ensure(ctx, ctx->mx[2], (size_t)S * M * E * 4));
-    RC(mixer_mgm(ctx, image, S, n_mod, (float*)ctx->mx[2].p, prec));
-    return mixer_cap(ctx, (const float*)ctx->mx[2].p, S, M, tokens, prec);
+    const bool tb = bf && E == 192 && (D / 2) % 32 == 0;  // bf16 intermediate tokens (half the HBM bytes)
+    RC(mixer_mgm(ctx, image, S, n_mod, ctx->mx[2].p, prec, tb));
+    return mixer_cap(ctx, ctx->mx[2].p, S, M, tokens, prec, tb);
   }
   if (d.mixer_type == MMPFN_MIXER_MOE) {
     const int ne = d.mgm_heads;

@@ -115,31 +115,28 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
 
     // ---- Q^T, K^T (C^T tiles) of the row, K = 192 in 6 steps (V after, to bound live registers)
     X8 qf[NT], kf[NT];
-    {
-      f32x4 qa[2][NT], ka[2][NT];
+    // Q then K, one set of 2 NT accumulators live at a time (both at once: 54 / 44 spills in the fp16 / bf16
+    // forms vs 46 / 24, and 2.5 / 4.5 % slower, profiles/r04/ab_feat_rows_qk_split.txt)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      f32x4 qa[2][NT];
 #pragma unroll
       for (int f = 0; f < 2; ++f)
 #pragma unroll
-        for (int tt = 0; tt < NT; ++tt) qa[f][tt] = ka[f][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int tt = 0; tt < NT; ++tt) qa[f][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < FR_E / 32; ++ks) {
-        X8 wqf[2], wkf[2];
+        X8 wqf[2];
 #pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          wqf[f] = *(const X8*)(wq + (16 * f + n) * FR_ST + 32 * ks + 8 * g);
-          wkf[f] = *(const X8*)(wq + (32 + 16 * f + n) * FR_ST + 32 * ks + 8 * g);
-        }
+        for (int f = 0; f < 2; ++f) wqf[f] = *(const X8*)(wq + (32 * j + 16 * f + n) * FR_ST + 32 * ks + 8 * g);
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
-          for (int f = 0; f < 2; ++f) {
-            qa[f][tt] = mfma16x(wqf[f], xf[tt][ks], qa[f][tt]);
-            ka[f][tt] = mfma16x(wkf[f], xf[tt][ks], ka[f][tt]);
-          }
+          for (int f = 0; f < 2; ++f) qa[f][tt] = mfma16x(wqf[f], xf[tt][ks], qa[f][tt]);
       }
 #pragma unroll
-      for (int tt = 0; tt < NT; ++tt)
-        qf[tt] = cat8<X8>(qa[0][tt], qa[1][tt]), kf[tt] = cat8<X8>(ka[0][tt], ka[1][tt]);
+      for (int tt = 0; tt < NT; ++tt) (j == 0 ? qf[tt] : kf[tt]) = cat8<X8>(qa[0][tt], qa[1][tt]);
+      __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_sched_barrier(0);  // phases in order: bounds the live registers (2 waves / SIMD)
     // ---- V (C tiles: lane = head dim, 4 consecutive tokens) -> V^T A fragments per key-tile pair

@@ -530,6 +530,105 @@ __global__ __launch_bounds__(512, 1) void gemm_glu_big_kernel(const bf16* __rest
   }
 }
 
+
+// ---------------------------------------------------------------- large-tile MGM down-projection (bf16)
+// Per head z (transformer.py:52-55: Linear(D/2 -> E) after the GLU): C[(s, z, mod)][E] = A[r][z D/2 + k] .
+// W2[z][E][k]^T + b2[z], the rows remapped head-major into the [S][mgm n_mod][E] token tensor.  The 64 x 192
+// tile of gemm_kernel re-reads its W (one head's 192 x 384) per 64 rows and runs at the L2 -> LDS fill
+// rate (75 us at PAD-UFES size); here 320 rows x the head's 192 outputs per 512-thread block (8 waves as
+// 2 x 4, each 160 x 48 = 10 x 3 MFMA-16 tiles), the same four-stage LDS-DMA ring and swizzled 64-B rows
+// as the GLU kernel (320 + 192 = 512 rows: four 16-B pieces per thread and slice), the M tiles of one
+// head back to back on one XCD.
+constexpr int GR_M = 320, GR_N = 192;
+static_assert(GR_M + GR_N == GB_M + GB_N, "four DMA pieces per thread and K slice, as the GLU kernel");
+constexpr int GR_MT = GR_M / 32;  // 16-row tiles per wave (10)
+constexpr int GR_NT = GR_N / 64;  // 16-column tiles per wave (3)
+
+template <typename TO>  // fp32 tokens, or bf16 (the MGM+CAP chain's intermediate, read by the CAP K|V projection)
+__global__ __launch_bounds__(512, 1) void gemm_remap_big_kernel(const bf16* __restrict__ A, int64_t lda,
+                                                                const bf16* __restrict__ W,
+                                                                const float* __restrict__ bias, TO* __restrict__ C,
+                                                                int M, int K, int mtiles, int n_mod, int Mtok) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fg = lane >> 4;
+  int mt, z;
+  {
+    const int nb = gridDim.x;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int per = nb >> 3, extra = nb & 7;
+    const int t = xcd * per + min(xcd, extra) + slot;
+    z = t / mtiles, mt = t - z * mtiles;
+  }
+  const int m0 = mt * GR_M;
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
+  const bf16* src[GB_DMA];
+#pragma unroll
+  for (int j = 0; j < GB_DMA; ++j) {
+    const int q = (wave * GB_DMA + j) * 64 + lane, r = q >> 2, c = gb_slot(r, q & 3);
+    src[j] = r < GR_M ? A + (int64_t)min(m0 + r, M - 1) * lda + (int64_t)z * K + c * 8
+                      : W + ((int64_t)z * GR_N + (r - GR_M)) * K + c * 8;
+  }
+  auto dma = [&](int kt) {
+    const unsigned base = lds0 + (kt % GB_NST) * GB_STAGE + wave * GB_DMA * 1024;
+#pragma unroll
+    for (int j = 0; j < GB_DMA; ++j)
+      gb_dma16(src[j] + kt * GB_K, __builtin_amdgcn_readfirstlane(base + j * 1024));
+  };
+  f32x4 acc[GR_MT][GR_NT];
+#pragma unroll
+  for (int a = 0; a < GR_MT; ++a)
+#pragma unroll
+    for (int b = 0; b < GR_NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = K / GB_K;
+#pragma unroll
+  for (int i = 0; i < GB_NST - 1; ++i)
+    if (i < nk) dma(i);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(nk - 1 - kt, GB_NST - 2);
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GB_DMA) : "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GB_DMA) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB_DMA) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + GB_NST - 1 < nk) dma(kt + GB_NST - 1);
+    const unsigned char* As = smem + (kt % GB_NST) * GB_STAGE;
+    const unsigned char* Ws = As + GR_M * GB_ROW;
+    bf16x8 af[GR_MT], bw[GR_NT];
+#pragma unroll
+    for (int i = 0; i < GR_NT; ++i) {
+      const int rb = wn * (GR_N / 4) + i * 16 + fr;
+      bw[i] = *(const bf16x8*)(Ws + rb * GB_ROW + 16 * gb_slot(rb, fg));
+    }
+#pragma unroll
+    for (int i = 0; i < GR_MT; ++i) {
+      const int ra = wm * (GR_M / 2) + i * 16 + fr;
+      af[i] = *(const bf16x8*)(As + ra * GB_ROW + 16 * gb_slot(ra, fg));
+    }
+#pragma unroll
+    for (int a = 0; a < GR_MT; ++a)
+#pragma unroll
+      for (int b = 0; b < GR_NT; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bw[b], acc[a][b], 0, 0, 0);
+  }
+  // C tile lane layout: row 16a + 4fg + r, column 16b + fr of the wave's 160 x 48 block; + b2[z], row remap
+#pragma unroll
+  for (int b = 0; b < GR_NT; ++b) {
+    const int n = wn * (GR_N / 4) + b * 16 + fr;
+    const float bv = bias[z * GR_N + n];
+#pragma unroll
+    for (int a = 0; a < GR_MT; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * (GR_M / 2) + a * 16 + fg * 4 + r;
+        if (m < M) {
+          const int64_t dr = (int64_t)(m / n_mod) * Mtok + (int64_t)z * n_mod + m % n_mod;
+          C[dr * GR_N + n] = (TO)(acc[a][b][r] + bv);
+        }
+      }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool out_f32, int groups,
@@ -550,6 +649,22 @@ hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool ou
     return out_f32 ? launch_e<1, true, true>(a, epi, groups, st) : launch_e<1, true, false>(a, epi, groups, st);
   }
   return out_f32 ? launch_e<1, false, true>(a, epi, groups, st) : launch_e<1, false, false>(a, epi, groups, st);
+}
+
+hipError_t launch_gemm_remap_big(const void* A, int64_t lda, const void* W, const float* bias, void* C, bool c_bf16,
+                                 int M, int K, int nheads, int n_mod, int E, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (E != GR_N || K % GB_K != 0 || K <= 0 || nheads <= 0 || n_mod <= 0) return hipErrorInvalidValue;
+  const int mtiles = (M + GR_M - 1) / GR_M;
+  const int64_t nb = (int64_t)mtiles * nheads;
+  const int lds = GB_NST * GB_STAGE;
+  if (c_bf16)
+    hipLaunchKernelGGL((gemm_remap_big_kernel<bf16>), dim3((unsigned)nb), dim3(512), lds, st, (const bf16*)A, lda,
+                       (const bf16*)W, bias, (bf16*)C, M, K, mtiles, n_mod, nheads * n_mod);
+  else
+    hipLaunchKernelGGL((gemm_remap_big_kernel<float>), dim3((unsigned)nb), dim3(512), lds, st, (const bf16*)A, lda,
+                       (const bf16*)W, bias, (float*)C, M, K, mtiles, n_mod, nheads * n_mod);
+  return hipGetLastError();
 }
 
 hipError_t launch_gemm_glu_big(const void* A, const void* W, const float* bias, void* C, int M, int N, int K,

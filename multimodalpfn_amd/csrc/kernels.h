@@ -82,6 +82,10 @@ hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool ou
 
 // MGM head bank, bf16: C[M][N/2] = GLU(A[M][K] . W^T + bias) with W rows GLU-interleaved in 16-row
 // blocks (capi.cpp); large-tile, XCD-ordered (gemm.hip gemm_glu_big_kernel); N % 256 == 0, K % 64 == 0
+// MGM per-head down-projection (bf16, E = 192): C[(r / n_mod) * nheads n_mod + z n_mod + r % n_mod][E] =
+// A[r][z K .. z K + K) (row stride lda) . W[z][E][K]^T + bias[z][E]; C fp32 or bf16 (c_bf16)
+hipError_t launch_gemm_remap_big(const void* A, int64_t lda, const void* W, const float* bias, void* C, bool c_bf16,
+                                 int M, int K, int nheads, int n_mod, int E, hipStream_t st);
 hipError_t launch_gemm_glu_big(const void* A, const void* W, const float* bias, void* C, int M, int N, int K,
                                hipStream_t st);
 
@@ -113,11 +117,11 @@ hipError_t launch_rowgemm_qkv_pair(const void* X, int64_t rdiv1, int64_t roff1, 
                                    int64_t rdiv2, int64_t roff2, const void* W2, int M2, int N2, int64_t a_rmul,
                                    void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st,
                                    bool f16 = false);
-// C = (ln ? LayerNorm(A) : A) . W^T + bias: A fp32 [M][192], W [N][192] bf16, C bf16 [M][N], N % 64 == 0;
+// C = (ln ? LayerNorm(A) : A) . W^T + bias: A fp32 or bf16 [M][192], W [N][192] bf16, C bf16 [M][N], N % 64 == 0;
 // with CT: outputs [vt_from, N) transposed per group of Mk rows into CT [M / Mk][N - vt_from][Mk] (Mk % 32 == 0),
 // C then [M][vt_from]
-hipError_t launch_rowgemm_ln_store(const float* A, const void* W, const float* bias, void* C, int64_t M, int N,
-                                   float eps, bool ln, hipStream_t st, void* CT = nullptr, int vt_from = -1,
+hipError_t launch_rowgemm_ln_store(const void* A, bool a_bf16, const void* W, const float* bias, void* C, int64_t M,
+                                   int N, float eps, bool ln, hipStream_t st, void* CT = nullptr, int vt_from = -1,
                                    int Mk = 0);
 hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, void* X, float eps, hipStream_t st,
                                 bool f16 = false);

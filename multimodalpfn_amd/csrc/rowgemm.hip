@@ -321,7 +321,8 @@ __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p, in
 // the QKV kernel above.  vt_from >= 0: outputs [vt_from, N) go transposed per group of Mk rows
 // (Mk % 32 == 0), CT [M / Mk][N - vt_from][Mk] (the CAP V^T: keys contiguous), the rest to C with
 // row stride ldc.
-__global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const float* __restrict__ A, const bf16* __restrict__ W,
+template <typename TA>
+__global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const TA* __restrict__ A, const bf16* __restrict__ W,
                                                                   const float* __restrict__ bias, bf16* __restrict__ C,
                                                                   int M, int N, float eps, int do_ln, int ldc,
                                                                   bf16* __restrict__ CT, int vt_from, int Mk) {
@@ -351,12 +352,18 @@ __global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const float* _
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const int64_t m = min(m0 + tt * 16 + fr, (int64_t)M - 1);
-    const float* xr = A + m * GE + fg * 8;
+    const TA* xr = A + m * GE + fg * 8;
     f32x4 lo[GE / 32], hi[GE / 32];
 #pragma unroll
     for (int ks = 0; ks < GE / 32; ++ks) {
-      lo[ks] = *(const f32x4*)(xr + ks * 32);
-      hi[ks] = *(const f32x4*)(xr + ks * 32 + 4);
+      if constexpr (sizeof(TA) == 2) {
+        const bf16x8 v = *(const bf16x8*)(xr + ks * 32);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lo[ks][i] = (float)v[i], hi[ks][i] = (float)v[4 + i];
+      } else {
+        lo[ks] = *(const f32x4*)(xr + ks * 32);
+        hi[ks] = *(const f32x4*)(xr + ks * 32 + 4);
+      }
     }
     float mean = 0.f, inv = 1.f;
     if (do_ln) {  // the row's 192 features are spread over lanes fr + 16 fg (48 each)
@@ -585,16 +592,20 @@ hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, void* X
   return hipGetLastError();
 }
 
-hipError_t launch_rowgemm_ln_store(const float* A, const void* W, const float* bias, void* C, int64_t M, int N,
-                                   float eps, bool ln, hipStream_t st, void* CT, int vt_from, int Mk) {
+hipError_t launch_rowgemm_ln_store(const void* A, bool a_bf16, const void* W, const float* bias, void* C, int64_t M,
+                                   int N, float eps, bool ln, hipStream_t st, void* CT, int vt_from, int Mk) {
   if (M <= 0) return hipSuccess;
   if (N % QC != 0 || N <= 0 || M > INT32_MAX) return hipErrorInvalidValue;
   if (CT && (vt_from < 0 || vt_from % QC != 0 || vt_from >= N || Mk <= 0 || Mk % 32 != 0 || M % Mk != 0))
     return hipErrorInvalidValue;
   const int ldc = CT ? vt_from : N;
-  hipLaunchKernelGGL(rowgemm_ln_store_kernel, dim3((unsigned)((M + GROWS - 1) / GROWS)), dim3(256), 0, st, A,
-                     (const bf16*)W, bias, (bf16*)C, (int)M, N, eps, ln ? 1 : 0, ldc, (bf16*)CT, CT ? vt_from : -1,
-                     CT ? Mk : 1);
+  const dim3 grid((unsigned)((M + GROWS - 1) / GROWS));
+  if (a_bf16)
+    hipLaunchKernelGGL((rowgemm_ln_store_kernel<bf16>), grid, dim3(256), 0, st, (const bf16*)A, (const bf16*)W, bias,
+                       (bf16*)C, (int)M, N, eps, ln ? 1 : 0, ldc, (bf16*)CT, CT ? vt_from : -1, CT ? Mk : 1);
+  else
+    hipLaunchKernelGGL((rowgemm_ln_store_kernel<float>), grid, dim3(256), 0, st, (const float*)A, (const bf16*)W, bias,
+                       (bf16*)C, (int)M, N, eps, ln ? 1 : 0, ldc, (bf16*)CT, CT ? vt_from : -1, CT ? Mk : 1);
   return hipGetLastError();
 }
 
