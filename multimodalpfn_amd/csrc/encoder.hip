@@ -106,6 +106,7 @@ __global__ __launch_bounds__(256) void enc_stats_kernel(const float* __restrict_
   const int tid = threadIdx.x;
   if ((int)blockIdx.x == nslots) {  // label mean
     double a[2] = {0.0, 0.0};
+#pragma unroll 16  // (independent loads in flight: a rolled loop waits out one memory latency per row)
     for (int s = tid; s < ny; s += 256) {
       const float v = y[s];
       if (!isnan(v)) a[0] += v, a[1] += 1.0;
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(256) void enc_stats_kernel(const float* __restrict_
   };
   if (col_lds) {
     const int n = S * fpg;
-#pragma unroll 8
+#pragma unroll 32  // (all of a typical column's loads in flight at once)
     for (int i = tid; i < n; i += 256) {
       const int s = i / fpg, j = i - s * fpg, c = g * fpg + j;
       cols[j * S + s] = c < F ? x[(int64_t)s * F + c] : 0.f;
