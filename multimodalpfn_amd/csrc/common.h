@@ -108,6 +108,20 @@ __device__ __forceinline__ float gelu_tanh_fast(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
 }
 
+// the same tanh form on a pair of fp16 values in packed 16-bit arithmetic (fp16 mode, whose hidden
+// activations are fp16 MFMA operands anyway): v_pk_mul / v_pk_fma / v_pk_add_f16 take one issue slot per
+// pair where the fp32 form takes one per element; v_exp_f16 / v_rcp_f16 per element.  2^u overflowing fp16
+// (x < -5.6) gives rcp(inf) = 0, x * 0 = 0, and underflow gives x: GELU's own limits.
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
+__device__ __forceinline__ f16x2_t gelu_tanh_h2(f16x2_t x) {
+  constexpr float k = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+  const f16x2_t kk = {(_Float16)k, (_Float16)k}, kc = {(_Float16)(k * 0.044715f), (_Float16)(k * 0.044715f)};
+  const f16x2_t one = {(_Float16)1.0f, (_Float16)1.0f};
+  const f16x2_t u = x * __builtin_elementwise_fma(kc, x * x, kk);
+  const f16x2_t d = f16x2_t{(_Float16)__builtin_exp2f16(u[0]), (_Float16)__builtin_exp2f16(u[1])} + one;
+  return x * f16x2_t{(_Float16)__builtin_amdgcn_rcph(d[0]), (_Float16)__builtin_amdgcn_rcph(d[1])};
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // Reductions over the four 16-lane rows of an MFMA C fragment (lanes l, l^16, l^32, l^48):

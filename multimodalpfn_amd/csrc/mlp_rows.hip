@@ -316,6 +316,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
 
   // GELU of one adjacent pair q (0 .. 4 TT - 1: tile tt, half ht, elements 2 (q & 1) + 0, 1) of a chunk's
   // H^T accumulators, packed into its bf16 B fragment for the down-projection
+#ifndef MLP_GELU16
+#define MLP_GELU16 1
+#endif
   auto gelu_pair = [&](auto qc, const f32x4 (&hs)[2][TT], X8 (&hb)[TT], int c) {
     constexpr int q = decltype(qc)::value, tt = q >> 2, ht = (q >> 1) & 1, i = 2 * (q & 1);
     HT2 pr;
@@ -323,6 +326,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
       const float2_t bb = *(const float2_t*)(capl + RE + c * RHC + 16 * ht + 4 * fg + i);
       pr = __builtin_convertvector((float2_t){gelu_erf(hs[ht][tt][i] + bb[0]), gelu_erf(hs[ht][tt][i + 1] + bb[1])},
                                    HT2);
+    } else if constexpr (F16 && MLP_GELU16) {  // fp16 mode: the pair's GELU in packed fp16 arithmetic
+      pr = gelu_tanh_h2(__builtin_convertvector((float2_t){hs[ht][tt][i], hs[ht][tt][i + 1]}, HT2));
     } else {
       pr = __builtin_convertvector((float2_t){gelu_tanh_fast(hs[ht][tt][i]), gelu_tanh_fast(hs[ht][tt][i + 1])}, HT2);
     }
@@ -389,6 +394,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     const bool MORE = c + 1 < nchunks;  // a chunk c+1 exists (wave-uniform)
     constexpr int PAR = decltype(parc)::value;
     [[maybe_unused]] const bool d1 = c + 3 < nchunks, d2 = c + 2 < nchunks;
+    // (issuing these six pieces one per k-step of the up-projection below, beside the GELU, measured
+    // neutral for fp16 and 1.5 % slower for bf16: profiles/r04/ab_mlp_gelu16_dma_spread.txt)
     if (d1) dma_w1(c + 3, PAR);
     if (d2) dma_w2(c + 2, (PAR + 2) % 3);
     // GELU of chunk c (VALU) inside the up-projection MFMAs of chunk c+1.  No branch on MORE: the last
