@@ -84,6 +84,19 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
       __builtin_amdgcn_global_load_lds(src + p * 512 + lane * 8, (lds_void*)(dst + p * 512), 16, 0, 0);
   };
 
+  // the same copy one piece at a time: piece i of this wave (wave + 4 i), clamped to the last piece so that
+  // the call is branch-free (a clamped piece rewrites the last piece's bytes with the same data)
+  auto dma_piece = [&](const void* srcv, void* dstv, int i) {
+    const int p = min(wave + 4 * i, FR_PIECES - 1);
+    __builtin_amdgcn_global_load_lds((const uint16_t*)srcv + p * 512 + lane * 8, (lds_void*)((uint16_t*)dstv + p * 512),
+                                     16, 0, 0);
+  };
+#ifndef FR_DMA_SPREAD
+#define FR_DMA_SPREAD 1
+#endif
+  constexpr int FR_PPW = (FR_PIECES + 3) / 4;  // pieces per wave (10)
+  constexpr bool SPREAD = FR_DMA_SPREAD && F16;  // the bf16 form: +16 spilled registers, not spread
+
   dma(pack, wbuf, FR_PIECES);  // head 0 -> buffer 0
   // ---- the row's tokens as bf16 fragments (padding tokens t >= T are zero)
   X8 xf[NT][FR_E / 32];
@@ -109,8 +122,13 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
   X8 of[FR_H][NT];  // O^T fragments of every head (K-step h of the out-projection)
 #pragma unroll
   for (int h = 0; h < FR_H; ++h) {
-    if (h + 1 < FR_H) dma(pack + (h + 1) * FR_QKV_IMG, wbuf + ((h + 1) & 1) * FR_QKV_IMG, FR_PIECES);
-    else dma(pack + FR_H * FR_QKV_IMG, wbuf, FR_PIECES);  // out-projection image, first half (buffer 0 is free)
+    // the next image: head h+1's QKV, or after the last head the out-projection image's first half (buffer 0
+    // is free); FR_DMA_SPREAD issues it one piece per k-step of the projections below instead of as one burst
+    // at the head's start (an LDS-DMA's issue cost grows with the other issues of its phase,
+    // MI355X_MICROARCH.md); the end-of-head barrier retires it either way
+    const WT* nsrc = h + 1 < FR_H ? pack + (h + 1) * FR_QKV_IMG : pack + FR_H * FR_QKV_IMG;
+    WT* ndst = h + 1 < FR_H ? wbuf + ((h + 1) & 1) * FR_QKV_IMG : wbuf;
+    if constexpr (!SPREAD) dma(nsrc, ndst, FR_PIECES);
     const WT* wq = wbuf + (h & 1) * FR_QKV_IMG;  // [96][FR_ST]: Q (permuted) | K (permuted) | V
 
     // ---- Q^T, K^T (C^T tiles) of the row, K = 192 in 6 steps (V after, to bound live registers)
@@ -133,6 +151,9 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
         for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
           for (int f = 0; f < 2; ++f) qa[f][tt] = mfma16x(wqf[f], xf[tt][ks], qa[f][tt]);
+        if constexpr (SPREAD) {  // pieces 0 .. 9 after the Q and K k-steps 0 .. 4 of each
+          if (ks < FR_PPW / 2) dma_piece(nsrc, ndst, j * (FR_PPW / 2) + ks);
+        }
       }
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) (j == 0 ? qf[tt] : kf[tt]) = cat8<X8>(qa[0][tt], qa[1][tt]);
@@ -205,6 +226,8 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
   }
   // second half of the out-projection image (buffer 1, read by head 5 until the barrier above)
   dma(pack + FR_H * FR_QKV_IMG + FR_QKV_IMG, wbuf + FR_QKV_IMG, FR_PIECES);
+  // (running token tile 0's output features 0 .. 95, buffer 0's rows, before this barrier measured neutral:
+  // 101.9 / 102.4 vs 101.3 / 101.9 µs, profiles/r04/ab_feat_rows_dma_spread.txt)
   __syncthreads();
 
   // ---- per token tile: Y^T = Wout . O^T over K = 192 (K-step h = head h), image [192][FR_ST],
