@@ -181,11 +181,14 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
   typedef typename Op16<F16>::t OT;  // Q / K element
   typedef typename Op16<F16>::x8 X8;
   typedef typename Op16<F16>::x4 X4;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
   const int rd = (int)p.a_rdiv;
   const int b = bid / tiles_per_b;
   const int l0 = (bid - b * tiles_per_b) * GROWS + wave * 32;  // wave's first row inside column b
+  // all 32 of the wave's rows exist (wave-uniform): the chunk stores then run unguarded, so the loop body
+  // carries no exec-mask branches; only a column's last partial tile takes the guarded stores
+  const bool full = l0 + 32 <= rd;
   uint16_t* const Os = Ws + 2 * QCEL + wave * OWEL;
   const int nch = p.N / QC;
   const uint16_t* Wg = (const uint16_t*)p.W;
@@ -238,69 +241,77 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
   if (nch > 1) fetch(1);
   __syncthreads();
   const int pos0 = (int)p.a_roff + l0;  // attention position of the wave's row 0
-  for (int c = 0; c < nch; ++c) {
-    if (c + 1 < nch) stash((c + 1) & 1);
-    if (c + 2 < nch) fetch(c + 2);
-    const uint16_t* W = Ws + (c & 1) * QCEL;
-    const int n0 = c * QC, j = n0 / GE;  // 0 q, 1 k, 2 v
-    const int h0 = (n0 - j * GE) >> 5;   // first of the chunk's two heads
-    f32x4 acc[QC / 16][2];
-#pragma unroll
-    for (int f = 0; f < QC / 16; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (j < 2) {
-      chunk_mma<true>(W, af, fr, fg, acc);
-      // C^T: lane = row 16tt + fr, features 16f + 4fg + i  ->  Os[row][feature]
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int f = 0; f < QC / 16; ++f) {
-          X4 o;
-          o[0] = (OT)acc[f][tt][0], o[1] = (OT)acc[f][tt][1];
-          o[2] = (OT)acc[f][tt][2], o[3] = (OT)acc[f][tt][3];
-          *(X4*)(Os + (tt * 16 + fr) * OQST + f * 16 + fg * 4) = o;
-        }
-      uint16_t* base = j == 0 ? (uint16_t*)p.q + (((int64_t)b * p.H + h0) * p.S + pos0) * 32
-                              : (uint16_t*)p.k + (((int64_t)b * p.H + h0) * p.Npad + pos0) * 32;
-      const int64_t hstride = (int64_t)(j == 0 ? p.S : p.Npad) * 32;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int row = 16 * i + (lane >> 2), cc = lane & 3;
-          const u32x4 v = *(const u32x4*)(Os + row * OQST + hh * 32 + cc * 8);
-          if (l0 + row < rd) *(u32x4*)(base + hh * hstride + row * 32 + cc * 8) = v;
-        }
-    } else {
-      chunk_mma<false>(W, af, fr, fg, acc);
-      // C: lane = feature 16f + fr, rows 16tt + 4fg + i  ->  Os[feature][row]
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int f = 0; f < QC / 16; ++f) {
-          bf16x4 o;
-          o[0] = (bf16)acc[f][tt][0], o[1] = (bf16)acc[f][tt][1];
-          o[2] = (bf16)acc[f][tt][2], o[3] = (bf16)acc[f][tt][3];
-          *(bf16x4*)(Os + (f * 16 + fr) * OVST + tt * 16 + fg * 4) = o;
-        }
-      uint16_t* base = (uint16_t*)p.vt + ((int64_t)b * p.H + h0) * 32 * p.Npad + pos0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int feat = 16 * i + (lane >> 2), rr = (lane & 3) * 8;
-        const u32x4 v = *(const u32x4*)(Os + feat * OVST + rr);
-        uint16_t* dst = base + (int64_t)feat * p.Npad + rr;  // feature = (head - h0) * 32 + d
-        if (l0 + rr + 8 <= rd) {
-          *(u32x4*)dst = v;
-        } else {
-          typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
-          const u16x8 e = __builtin_bit_cast(u16x8, v);
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if (l0 + rr + k < rd) dst[k] = e[k];
+  auto run = [&](auto fullc) {
+    constexpr bool FULL = decltype(fullc)::value;
+    for (int c = 0; c < nch; ++c) {
+      if (c + 1 < nch) stash((c + 1) & 1);
+      if (c + 2 < nch) fetch(c + 2);
+      const uint16_t* W = Ws + (c & 1) * QCEL;
+      const int n0 = c * QC, j = n0 / GE;  // 0 q, 1 k, 2 v
+      const int h0 = (n0 - j * GE) >> 5;   // first of the chunk's two heads
+      f32x4 acc[QC / 16][2];
+  #pragma unroll
+      for (int f = 0; f < QC / 16; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (j < 2) {
+        chunk_mma<true>(W, af, fr, fg, acc);
+        // C^T: lane = row 16tt + fr, features 16f + 4fg + i  ->  Os[row][feature]
+  #pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+  #pragma unroll
+          for (int f = 0; f < QC / 16; ++f) {
+            X4 o;
+            o[0] = (OT)acc[f][tt][0], o[1] = (OT)acc[f][tt][1];
+            o[2] = (OT)acc[f][tt][2], o[3] = (OT)acc[f][tt][3];
+            *(X4*)(Os + (tt * 16 + fr) * OQST + f * 16 + fg * 4) = o;
+          }
+        uint16_t* base = j == 0 ? (uint16_t*)p.q + (((int64_t)b * p.H + h0) * p.S + pos0) * 32
+                                : (uint16_t*)p.k + (((int64_t)b * p.H + h0) * p.Npad + pos0) * 32;
+        const int64_t hstride = (int64_t)(j == 0 ? p.S : p.Npad) * 32;
+  #pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+  #pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int row = 16 * i + (lane >> 2), cc = lane & 3;
+            const u32x4 v = *(const u32x4*)(Os + row * OQST + hh * 32 + cc * 8);
+            if (FULL || l0 + row < rd) *(u32x4*)(base + hh * hstride + row * 32 + cc * 8) = v;
+          }
+      } else {
+        chunk_mma<false>(W, af, fr, fg, acc);
+        // C: lane = feature 16f + fr, rows 16tt + 4fg + i  ->  Os[feature][row]
+  #pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+  #pragma unroll
+          for (int f = 0; f < QC / 16; ++f) {
+            bf16x4 o;
+            o[0] = (bf16)acc[f][tt][0], o[1] = (bf16)acc[f][tt][1];
+            o[2] = (bf16)acc[f][tt][2], o[3] = (bf16)acc[f][tt][3];
+            *(bf16x4*)(Os + (f * 16 + fr) * OVST + tt * 16 + fg * 4) = o;
+          }
+        uint16_t* base = (uint16_t*)p.vt + ((int64_t)b * p.H + h0) * 32 * p.Npad + pos0;
+  #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int feat = 16 * i + (lane >> 2), rr = (lane & 3) * 8;
+          const u32x4 v = *(const u32x4*)(Os + feat * OVST + rr);
+          uint16_t* dst = base + (int64_t)feat * p.Npad + rr;  // feature = (head - h0) * 32 + d
+          if (FULL || l0 + rr + 8 <= rd) {
+            *(u32x4*)dst = v;
+          } else {
+            typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+            const u16x8 e = __builtin_bit_cast(u16x8, v);
+  #pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if (l0 + rr + k < rd) dst[k] = e[k];
+          }
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
-  }
+  };
+#ifndef QKV_VERSIONED
+#define QKV_VERSIONED 1
+#endif
+  if (QKV_VERSIONED && full) run(std::true_type{});
+  else run(std::false_type{});
 }
 
 // Two row sets in one launch: blocks [0, nblk1) project p's rows (the train rows: q|k|v), the
