@@ -140,6 +140,15 @@ __device__ __forceinline__ float max_rows4(float v) {
   return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
+// wave sum on DPP row operations + permlane swaps (no LDS round trip, unlike __shfl_xor's ds_bpermute);
+// every lane ends with the same value
+__device__ __forceinline__ float wave_sum_dpp_f(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));   // quad [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));   // quad [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xf, 0xf, false));  // row_mirror
+  return sum_rows4(v);
+}
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

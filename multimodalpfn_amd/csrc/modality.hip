@@ -261,6 +261,12 @@ constexpr float A64_TAU = 8.0f;
 constexpr int A64_STAGE = 2 * 8192 + 256;  // K [64][128 B] | V^T [64][128 B] | key bias [64] f32
 
 __device__ __forceinline__ int a64_off(int row, int c) { return row * 128 + 16 * (c ^ ((row >> 1) & 7)); }
+// V image: natural [key][d] rows (128 B, 16-B chunk c of row k at c ^ 4 ((k >> 1) & 1)), written with one
+// ds_write_b128 per 8 d's and read transposed by ds_read_b64_tr_b16 (a 4-key x 16-d block per 16 lanes,
+// MI355X / cdna_hip_programming.md T10): the swizzle makes the four key rows of a read land on four
+// different 16-dword bank ranges, so each 32-lane half is conflict-free
+__device__ __forceinline__ int a64v_off(int key, int c) { return key * 128 + 16 * (c ^ (((key >> 1) & 1) << 2)); }
+typedef short a64_s4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__ qkv, const float* __restrict__ kbias,
                                                         bf16* __restrict__ out, int L, int H, int q0, int nq,
@@ -321,15 +327,7 @@ __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__
     for (int i = 0; i < 2; ++i) {
       const int cidx = tid + 256 * i, key = cidx >> 3, ch = cidx & 7;
       *(u32x4*)(Ks + a64_off(key, ch)) = rk[i];
-      // V^T: d = 8 ch + e, key position in its 16-key group per the P fragment order
-      const int g = key >> 4, kk = key & 15;
-      const int kh = (kk >> 2) & 1, j = (kk & 3) + 4 * (kk >> 3);
-      const bf16x8 e = __builtin_bit_cast(bf16x8, rv[i]);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int d = 8 * ch + t;
-        *(bf16*)(Vs + a64_off(d, 2 * g + kh) + 2 * j) = e[t];
-      }
+      *(u32x4*)(Vs + a64v_off(key, ch)) = rv[i];  // V as stored: [key][d]
     }
     if (tid < 64) ((float*)(Ks + 16384))[tid] = rb;
   };
@@ -403,11 +401,25 @@ __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__
           s[1][i] -= delta;
         }
       }
+      // V^T A fragments (lane: d = 32 db + (lane & 31); elements j: keys b + (j & 3) + 8 (j >> 2), b = 16 ks + 4 hh,
+      // the P fragment's key order) as two transposed 4-key reads; lane 4q + p of each 16-lane group addresses
+      // key b + q (+ 8), d's 16 ((lane >> 4) & 1) + 4p .. +3 of its block (active is wave-uniform: EXEC is full)
       bf16x8 vf[2][4];
+      {
+        const int q = (lane & 15) >> 2, p4 = lane & 3, dh = (lane >> 4) & 1;
 #pragma unroll
-      for (int db = 0; db < 2; ++db)
+        for (int db = 0; db < 2; ++db)
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) vf[db][ks] = *(const bf16x8*)(Vs + a64_off(32 * db + r, 2 * ks + hh));
+          for (int ks = 0; ks < 4; ++ks) {
+            const int kb = 16 * ks + 4 * hh + q, c = 4 * db + 2 * dh + (p4 >> 1);
+            const a64_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) a64_s4*)(Vs + a64v_off(kb, c) + 8 * (p4 & 1)));
+            const a64_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) a64_s4*)(Vs + a64v_off(kb + 8, c) + 8 * (p4 & 1)));
+            const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
+            vf[db][ks] = bf16x8{l4[0], l4[1], l4[2], l4[3], h4[0], h4[1], h4[2], h4[3]};
+          }
+      }
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -531,7 +543,7 @@ __global__ __launch_bounds__(256) void ln_dual_kernel(const float* in, int64_t r
     v[j] = i4 < n4 ? *(const f32x4*)(x + 4 * i4) : f32x4{0.f, 0.f, 0.f, 0.f};
     s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
   }
-  const float mean = wave_sum(s) / dim;
+  const float mean = wave_sum_dpp_f(s) / dim;
   float q = 0.f;
 #pragma unroll
   for (int j = 0; j < V4; ++j)
@@ -541,20 +553,17 @@ __global__ __launch_bounds__(256) void ln_dual_kernel(const float* in, int64_t r
         const float d = v[j][e] - mean;
         q += d * d;
       }
-  const float inv = 1.0f / sqrtf(wave_sum(q) / dim + eps);
+  const float inv = 1.0f / sqrtf(wave_sum_dpp_f(q) / dim + eps);
 #pragma unroll
   for (int j = 0; j < V4; ++j) {
     const int i4 = lane + 64 * j;
     if (i4 >= n4) continue;
+    // gamma / beta as 16-B loads (dim % 4 == 0), not 4-B loads per element
+    const f32x4 gv = g ? *(const f32x4*)(g + 4 * i4) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 bv = bta ? *(const f32x4*)(bta + 4 * i4) : f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 y;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int i = 4 * i4 + e;
-      float t = (v[j][e] - mean) * inv;
-      if (g) t *= g[i];
-      if (bta) t += bta[i];
-      y[e] = t;
-    }
+    for (int e = 0; e < 4; ++e) y[e] = (v[j][e] - mean) * inv * gv[e] + bv[e];
     if (out32) *(f32x4*)(out32 + row * out_rstride + 4 * i4) = y;
     if (out16) {
       bf16x4 w;
