@@ -268,6 +268,12 @@ __device__ __forceinline__ int a64_off(int row, int c) { return row * 128 + 16 *
 __device__ __forceinline__ int a64v_off(int key, int c) { return key * 128 + 16 * (c ^ (((key >> 1) & 1) << 2)); }
 typedef short a64_s4 __attribute__((ext_vector_type(4)));
 
+// NCH query chains of 32 per wave (block = 4 waves x 32 NCH queries): with two, one chain's exps issue
+// beside the other chain's MFMAs inside one basic block (the per-chain lazy rescales are decided before it)
+#ifndef A64_NCH
+#define A64_NCH 2
+#endif
+template <int NCH>
 __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__ qkv, const float* __restrict__ kbias,
                                                         bf16* __restrict__ out, int L, int H, int q0, int nq,
                                                         int64_t o_bstride, int chunks, int nblocks) {
@@ -285,20 +291,22 @@ __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__
     const int bh = task / chunks;
     h = bh % H, b = bh / H;
   }
-  const int qw = chunk * 128 + wave * 32;  // first query (relative to q0) of this wave
-  const bool active = qw < nq;             // wave-uniform
-  const int qi = qw + r;
-  const int qt = q0 + min(qi, nq - 1);
+  const int qw = chunk * (128 * NCH) + wave * (32 * NCH);  // first query (relative to q0) of this wave
+  const bool active = qw < nq;                             // wave-uniform
   const bf16* base = qkv + (int64_t)b * L * ld;
   const float c = kLog2e * 0.125f;  // log2(e) / sqrt(64)
-  bf16x8 qf[4];
-  {
+  int qi[NCH];
+  bf16x8 qf[NCH][4];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    qi[ch] = qw + 32 * ch + r;
+    const int qt = q0 + min(qi[ch], nq - 1);
     const bf16* qrow = base + (int64_t)qt * ld + h * 64;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const bf16x8 raw = *(const bf16x8*)(qrow + 16 * ks + 8 * hh);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) qf[ks][e] = (bf16)((float)raw[e] * c);
+      for (int e = 0; e < 8; ++e) qf[ch][ks][e] = (bf16)((float)raw[e] * c);
     }
   }
   const float* kb = kbias ? kbias + (int64_t)b * L : nullptr;
@@ -339,12 +347,19 @@ __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__
 #pragma unroll
     for (int j = 0; j < 8; ++j) sel[j] = (bf16)(one ? 1.0f : 0.0f);
   }
-  f32x16 o[2], negm;
-  f32x4 lacc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < 16; ++i) o[0][i] = o[1][i] = negm[i] = 0.f;
+  // one reference max for the wave's NCH chains (as for the 32 queries of a chain: a wave-wide reference)
+  f32x16 o[NCH][2], negm;
+  f32x4 lacc[NCH];
   float mref = 0.f;
   bool have_m = false;  // mref set (a tile with an unmasked key seen)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) negm[i] = 0.f;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[ch][0][i] = o[ch][1][i] = 0.f;
+    lacc[ch] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   const int ntiles = (L + A64_KT - 1) / A64_KT;
 
   gload(0);
@@ -362,25 +377,32 @@ __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) kf[u][ks] = *(const bf16x8*)(Ks + a64_off(32 * u + r, 2 * ks + hh));
-      f32x16 s[2];
+      f32x16 s[NCH][2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        s[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qf[0], negm, 0, 0, 0);
+      for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
-        for (int ks = 1; ks < 4; ++ks) s[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][ks], qf[ks], s[u], 0, 0, 0);
-      }
+        for (int u = 0; u < 2; ++u) {
+          s[ch][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qf[ch][0], negm, 0, 0, 0);
+#pragma unroll
+          for (int ks = 1; ks < 4; ++ks)
+            s[ch][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][ks], qf[ch][ks], s[ch][u], 0, 0, 0);
+        }
       if (kbias != nullptr || (it == ntiles - 1 && (L % A64_KT) != 0)) {  // key bias and keys past L (0 / -inf)
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const float bv = Bs[32 * u + (i & 3) + 8 * (i >> 2) + 4 * hh];
-            s[u][i] = bv == 0.f ? s[u][i] : (bv == -INFINITY ? -INFINITY : s[u][i] + bv * kLog2e);
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch)
+              s[ch][u][i] = bv == 0.f ? s[ch][u][i] : (bv == -INFINITY ? -INFINITY : s[ch][u][i] + bv * kLog2e);
           }
       }
-      float tm = fmaxf(s[0][0], s[1][0]);
+      float tm = -INFINITY;
 #pragma unroll
-      for (int i = 1; i < 16; ++i) tm = fmaxf(tm, fmaxf(s[0][i], s[1][i]));
+      for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tm = fmaxf(tm, fmaxf(s[ch][0][i], s[ch][1][i]));
       {
         const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tm), __float_as_uint(tm), false, false);
         tm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
@@ -389,17 +411,21 @@ __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__
         const float delta = !have_m ? (tm == -INFINITY ? 0.f : tm) : fmaxf(tm, 0.f);
         have_m = have_m || tm != -INFINITY;
         const float alpha = exp2f(-delta);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[0][i] *= alpha, o[1][i] *= alpha;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) lacc[i] *= alpha;
         mref += delta;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          negm[i] = -mref;
-          s[0][i] -= delta;
-          s[1][i] -= delta;
+        for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[ch][0][i] *= alpha, o[ch][1][i] *= alpha;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) lacc[ch][i] *= alpha;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            s[ch][0][i] -= delta;
+            s[ch][1][i] -= delta;
+          }
         }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) negm[i] = -mref;
       }
       // V^T A fragments (lane: d = 32 db + (lane & 31); elements j: keys b + (j & 3) + 8 (j >> 2), b = 16 ks + 4 hh,
       // the P fragment's key order) as two transposed 4-key reads; lane 4q + p of each 16-lane group addresses
@@ -411,46 +437,52 @@ __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__
         for (int db = 0; db < 2; ++db)
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
-            const int kb = 16 * ks + 4 * hh + q, c = 4 * db + 2 * dh + (p4 >> 1);
+            const int kb = 16 * ks + 4 * hh + q, cc = 4 * db + 2 * dh + (p4 >> 1);
             const a64_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) a64_s4*)(Vs + a64v_off(kb, c) + 8 * (p4 & 1)));
+                (__attribute__((address_space(3))) a64_s4*)(Vs + a64v_off(kb, cc) + 8 * (p4 & 1)));
             const a64_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) a64_s4*)(Vs + a64v_off(kb + 8, c) + 8 * (p4 & 1)));
+                (__attribute__((address_space(3))) a64_s4*)(Vs + a64v_off(kb + 8, cc) + 8 * (p4 & 1)));
             const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
             vf[db][ks] = bf16x8{l4[0], l4[1], l4[2], l4[3], h4[0], h4[1], h4[2], h4[3]};
           }
       }
+      // chain by chain (a chain's scores die after its P.V): the next chain's exps issue beside this chain's MFMAs
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
-        for (int sp = 0; sp < 2; ++sp) {
-          bf16x8 pb;
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) pb[j] = (bf16)__builtin_amdgcn_exp2f(s[u][8 * sp + j]);
-          const int ks = 2 * u + sp;
-          o[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0][ks], pb, o[0], 0, 0, 0);
-          o[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[1][ks], pb, o[1], 0, 0, 0);
-          lacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc, 0, 0, 0);
-        }
+          for (int sp = 0; sp < 2; ++sp) {
+            bf16x8 pb;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pb[j] = (bf16)__builtin_amdgcn_exp2f(s[ch][u][8 * sp + j]);
+            const int ks = 2 * u + sp;
+            o[ch][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0][ks], pb, o[ch][0], 0, 0, 0);
+            o[ch][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[1][ks], pb, o[ch][1], 0, 0, 0);
+            lacc[ch] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[ch], 0, 0, 0);
+          }
     }
     if (it + 1 < ntiles) lstore((it + 1) & 1);
     __syncthreads();
   }
   if (!active) return;
-  const float la = __shfl(lacc[0], lane & 15, 64), lb = __shfl(lacc[1], lane & 15, 64);
-  const float ls = r < 16 ? la : lb;
-  const float inv = ls > 0.f ? 1.0f / ls : 0.f;  // a query with every key masked gets 0
-  if (qi < nq) {
-    bf16* orow = out + ((int64_t)b * o_bstride + qi) * D + h * 64;
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
+  for (int ch = 0; ch < NCH; ++ch) {
+    const float la = __shfl(lacc[ch][0], lane & 15, 64), lb = __shfl(lacc[ch][1], lane & 15, 64);
+    const float ls = r < 16 ? la : lb;
+    const float inv = ls > 0.f ? 1.0f / ls : 0.f;  // a query with every key masked gets 0
+    if (qi[ch] < nq) {
+      bf16* orow = out + ((int64_t)b * o_bstride + qi[ch]) * D + h * 64;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 w;
+      for (int db = 0; db < 2; ++db)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = (bf16)(o[db][4 * g + e] * inv);
-        *(bf16x4*)(orow + 32 * db + 8 * g + 4 * hh) = w;
-      }
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = (bf16)(o[ch][db][4 * g + e] * inv);
+          *(bf16x4*)(orow + 32 * db + 8 * g + 4 * hh) = w;
+        }
+    }
   }
 }
 
@@ -777,15 +809,19 @@ hipError_t launch_attn64(const void* qkv, const float* kbias, void* out, int B, 
                          int64_t o_bstride, int prec, hipStream_t st) {
   if (B <= 0 || nq <= 0) return hipSuccess;
   if (L <= 0 || H <= 0 || q0 < 0 || q0 + nq > L) return hipErrorInvalidValue;
-  const int chunks = (nq + 127) / 128;
-  const int64_t nb = (int64_t)B * H * chunks;
-  if (nb > 0x7fffffff) return hipErrorInvalidValue;
-  if (prec == PREC_BF16)
-    hipLaunchKernelGGL(attn64_kernel, dim3((unsigned)nb), dim3(256), 0, st, (const bf16*)qkv, kbias, (bf16*)out, L, H,
-                       q0, nq, o_bstride, chunks, (int)nb);
-  else
+  if (prec == PREC_BF16) {
+    const int chunks = (nq + 128 * A64_NCH - 1) / (128 * A64_NCH);
+    const int64_t nb = (int64_t)B * H * chunks;
+    if (nb > 0x7fffffff) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(attn64_kernel<A64_NCH>, dim3((unsigned)nb), dim3(256), 0, st, (const bf16*)qkv, kbias,
+                       (bf16*)out, L, H, q0, nq, o_bstride, chunks, (int)nb);
+  } else {
+    const int chunks = (nq + 127) / 128;
+    const int64_t nb = (int64_t)B * H * chunks;
+    if (nb > 0x7fffffff) return hipErrorInvalidValue;
     hipLaunchKernelGGL(attn64_f32_kernel, dim3((unsigned)nb), dim3(128), 0, st, (const float*)qkv, kbias, (float*)out,
                        L, H, q0, nq, o_bstride, chunks);
+  }
   return hipGetLastError();
 }
 
