@@ -110,8 +110,11 @@ def attn_traffic(T):
     """HBM bytes per attention launch over T token columns, from the committed PMC pass
     (tools/attn_pmc.sh: rocprofv3 FETCH_SIZE and WRITE_SIZE runs at that launch shape)."""
     H, d, S, N = 6, 32, S_ROWS, N_TRAIN
-    # the shipped kernel's own pass only (attn_pipe_kernel from round 3; older rounds measured attn_item2)
-    for pmc in sorted((ROOT / "profiles" / "r03").glob("attn_pipe_pmc_T*[0-9].json")):
+    # the shipped kernel's own pass only: the fp16 mode's launch (round 4) first, then the bf16 one (round 3;
+    # older rounds measured attn_item2)
+    cands = sorted((ROOT / "profiles" / "r04").glob("attn_pipe_pmc_T*_f16.json")) + \
+        sorted((ROOT / "profiles" / "r03").glob("attn_pipe_pmc_T*[0-9].json"))
+    for pmc in cands:
         rec = json.loads(pmc.read_text())
         if rec.get("shape") == {"T": T, "H": H, "d": d, "S": S, "N": N}:
             return rec["hbm_bytes_per_launch"], str(pmc.relative_to(ROOT))

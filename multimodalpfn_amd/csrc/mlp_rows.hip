@@ -312,10 +312,6 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     if (deep) wait_vm(integral_constant<int, (NW == 8 ? 2 : 4) * MP>{});
     else wait_vm(integral_constant<int, 0>{});
   }
-#ifdef MLP_NOFILL
-  if (nchunks > 2) dma_w2(2, 2);  // (finite weights in every slot)
-  wait_vm(integral_constant<int, 0>{});
-#endif
   __syncthreads();
 
   // GELU of one adjacent pair q (0 .. 4 TT - 1: tile tt, half ht, elements 2 (q & 1) + 0, 1) of a chunk's
@@ -400,10 +396,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     [[maybe_unused]] const bool d1 = c + 3 < nchunks, d2 = c + 2 < nchunks;
     // (issuing these six pieces one per k-step of the up-projection below, beside the GELU, measured
     // neutral for fp16 and 1.5 % slower for bf16: profiles/r04/ab_mlp_gelu16_dma_spread.txt)
-#ifndef MLP_NOFILL  // diagnostics only (timing): no ring refills after the prologue's
     if (d1) dma_w1(c + 3, PAR);
     if (d2) dma_w2(c + 2, (PAR + 2) % 3);
-#endif
     // GELU of chunk c (VALU) inside the up-projection MFMAs of chunk c+1.  No branch on MORE: the last
     // chunk's up-projection reads a slot holding an older chunk (landed, unused result), which costs 1/24
     // of the up-projections and measured 0.7 % faster than the branch (159.9 -> 158.8 us)

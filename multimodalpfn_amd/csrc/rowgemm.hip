@@ -239,18 +239,13 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
   }
   stash(0);
   if (nch > 1) fetch(1);
-#ifdef QKV_NOFILL
-  stash(1);  // (chunk 1's registers: finite weights in both slots)
-#endif
   __syncthreads();
   const int pos0 = (int)p.a_roff + l0;  // attention position of the wave's row 0
   auto run = [&](auto fullc) {
     constexpr bool FULL = decltype(fullc)::value;
     for (int c = 0; c < nch; ++c) {
-#ifndef QKV_NOFILL  // diagnostics only (timing): no weight refills, every chunk computes on slot 0 / 1 as left
       if (c + 1 < nch) stash((c + 1) & 1);
       if (c + 2 < nch) fetch(c + 2);
-#endif
       const uint16_t* W = Ws + (c & 1) * QCEL;
       const int n0 = c * QC, j = n0 / GE;  // 0 q, 1 k, 2 v
       const int h0 = (n0 - j * GE) >> 5;   // first of the chunk's two heads

@@ -13,4 +13,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 120 rocprofv3 --pmc $c -d $R/gpurun_out/apmc_$c -o run --output-format csv -- \
     python3 $R/tools/attn_time.py 5 > $R/gpurun_out/apmc_$c.log 2>&1 || exit 1
 done
-cd $R && python3 tools/attn_pmc_summary.py gpurun_out/apmc_FETCH_SIZE gpurun_out/apmc_WRITE_SIZE > gpurun_out/attn_pipe_pmc_T$ATT_T.json
+cd $R && python3 tools/attn_pmc_summary.py gpurun_out/apmc_FETCH_SIZE gpurun_out/apmc_WRITE_SIZE > gpurun_out/attn_pipe_pmc_T$ATT_T${ATT_PREC:+_$ATT_PREC}.json

@@ -20,10 +20,11 @@ fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
 write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
 read_b = 2.0 * fetch * 1024
 write_b = write * 1024
-alg_read = T * H * S * d * 2 + 2 * T * H * N * d * 2  # Q + K + V^T (bf16), keys up to nk
+alg_read = T * H * S * d * 2 + 2 * T * H * N * d * 2  # Q + K + V^T (16-bit), keys up to nk
 alg_write = T * S * H * d * 2
 print(json.dumps({
     "kernel": "attn_pipe_kernel",
+    "precision": os.environ.get("ATT_PREC", "bf16"),
     "shape": {"T": T, "H": H, "d": d, "S": S, "N": N},
     "launches": len(vals["FETCH_SIZE"]),
     "FETCH_SIZE_KiB_avg": round(fetch, 1),

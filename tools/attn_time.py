@@ -18,16 +18,23 @@ Npad = (N + 63) // 64 * 64
 lib = _lib.load_library(os.environ.get("MMPFN_LIB") or None)
 ctx = lib.mmpfn_create(0, None)
 g = torch.Generator().manual_seed(0)
-q = torch.randn(T, H, S, d, generator=g).cuda().bfloat16()
-k = torch.randn(T, H, Npad, d, generator=g).cuda().bfloat16()
+# ATT_PREC=f16: the fp16 mode's kernel (q, k, out fp16, V^T bf16; the headline's launch), else bf16
+f16 = os.environ.get("ATT_PREC", "bf16") == "f16"
+qdt = torch.float16 if f16 else torch.bfloat16
+q = torch.randn(T, H, S, d, generator=g).cuda().to(qdt)
+k = torch.randn(T, H, Npad, d, generator=g).cuda().to(qdt)
 vt = torch.randn(T, H, d, Npad, generator=g).cuda().bfloat16()
-o = torch.empty(T, S, H * d, device="cuda", dtype=torch.bfloat16)
+o = torch.empty(T, S, H * d, device="cuda", dtype=qdt)
 st = torch.cuda.current_stream()
 
 
-
 def launch():
-    rc = lib.mmpfn_item_attention_layer(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), S, T, H, Npad, N)
+    if f16:
+        rc = lib.mmpfn_item_attention_layer_ex(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), S, T, H,
+                                               Npad, N, 5)  # MMPFN_PREC_F16
+    else:
+        rc = lib.mmpfn_item_attention_layer(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), S, T, H,
+                                            Npad, N)
     assert rc == 0
 
 
