@@ -26,9 +26,9 @@ constexpr int TM = 256, TN = 256, TK = 32;
 constexpr int TROW = TK * 2;                    // 64-B LDS rows
 constexpr int TSTAGE = (TM + TN) * TROW;        // 32 KB per ring stage
 #ifndef GT_NST
-#define GT_NST 5
+#define GT_NST 4  // 5 (all 160 KB of LDS): ViT batch 20.52-20.55 vs 20.21 ms, profiles/r04/modality/ab_gemm_tile_variants.txt
 #endif
-constexpr int TNST = GT_NST;                    // ring stages (5 x 32 KB: three slices in flight)
+constexpr int TNST = GT_NST;                    // ring stages (4 x 32 KB: two slices in flight)
 constexpr int TDMA = (TM + TN) * (TROW / 16) / 512;  // 16-B DMA pieces per thread and slice (4)
 constexpr int TMT = TM / 32;                    // 16-row MFMA tiles per wave (8)
 constexpr int OST16 = TN + 8;                   // bf16 output staging row stride (elements)
