@@ -76,6 +76,14 @@ int mmpfn_vit_forward(mmpfn_enc* enc, const float* images, int B, int H, int W, 
 int mmpfn_text_forward(mmpfn_enc* enc, const int32_t* ids, const int32_t* mask, const int32_t* types, int B, int L,
                        float* cls, float* hidden, int precision);
 
+/* Kernel tap (tests, diagnostics): the towers' self-attention (layers/attention.py:58-77; the text tower's
+ * masked BERT attention) on device buffers: qkv [B][L][3][H][64] (the QKV GEMM's rows: q | k | v), kbias
+ * [B][L] fp32 additive key bias in natural-log units (-inf excludes the key) or NULL, out [B][L][H*64];
+ * bf16 qkv / out for MMPFN_PREC_BF16, fp32 for MMPFN_PREC_F32.  A query whose keys are all excluded gets 0.
+ * Runs on the encoder's stream; needs no model. */
+int mmpfn_enc_attention(mmpfn_enc* enc, const void* qkv, const float* kbias, void* out, int B, int L, int H,
+                        int precision);
+
 #ifdef __cplusplus
 }
 #endif

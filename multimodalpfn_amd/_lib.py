@@ -162,6 +162,7 @@ MODALITY_SIGNATURES = [
     ("mmpfn_enc_finalize", _i, [_vp]),
     ("mmpfn_vit_forward", _i, [_vp, _vp, _i, _i, _i, _vp, _vp, _i]),
     ("mmpfn_text_forward", _i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _i]),
+    ("mmpfn_enc_attention", _i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i]),
 ]
 
 _LIB = None

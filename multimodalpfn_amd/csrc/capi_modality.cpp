@@ -494,6 +494,16 @@ int mmpfn_vit_forward(mmpfn_enc* enc, const float* images, int B, int H, int W, 
   return MMPFN_OK;
 }
 
+int mmpfn_enc_attention(mmpfn_enc* enc, const void* qkv, const float* kbias, void* out, int B, int L, int H,
+                        int precision) {
+  if (!enc) return MMPFN_ERR_INVALID;
+  if (!qkv || !out || B <= 0 || L <= 0 || H <= 0) return fail(enc, MMPFN_ERR_INVALID, "qkv, out and B, L, H > 0");
+  if (precision != PREC_F32 && precision != PREC_BF16) return fail(enc, MMPFN_ERR_INVALID, "bad precision");
+  HIPCHK(hipSetDevice(enc->device));
+  HIPCHK(launch_attn64(qkv, kbias, out, B, L, H, 0, L, L, precision, enc->stream));
+  return MMPFN_OK;
+}
+
 int mmpfn_text_forward(mmpfn_enc* enc, const int32_t* ids, const int32_t* mask, const int32_t* types, int B, int L,
                        float* cls, float* hidden, int precision) {
   if (!enc) return MMPFN_ERR_INVALID;

@@ -350,13 +350,12 @@ __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__
 #pragma unroll
     for (int j = 0; j < 8; ++j) sel[j] = (bf16)(one ? 1.0f : 0.0f);
   }
-  // one reference max for the wave's NCH chains (as for the 32 queries of a chain: a wave-wide reference)
-  f32x16 o[NCH][2], negm;
+  // the re-run pass's running max, per chain and lane (= per query: lanes l and l + 32 hold one query's two key
+  // halves and agree after the permlane swap); a reference shared by two queries can leave one of them with
+  // underflowing sums, so each chain keeps its own
+  f32x16 o[NCH][2];
   f32x4 lacc[NCH];
-  float mref = 0.f;
-  bool have_m = false;  // mref set (a tile with an unmasked key seen)
-#pragma unroll
-  for (int i = 0; i < 16; ++i) negm[i] = 0.f;
+  const f32x16 zero16 = {};
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
 #pragma unroll
@@ -368,105 +367,146 @@ __global__ __launch_bounds__(256, 2) void attn64_kernel(const bf16* __restrict__
   gload(0);
   lstore(0);
   __syncthreads();
-  for (int it = 0; it < ntiles; ++it) {
-    const int k0 = it * A64_KT;
-    if (it + 1 < ntiles) gload(k0 + A64_KT);
-    const unsigned char* Ks = lds[it & 1];
-    const unsigned char* Vs = Ks + 8192;
-    const float* Bs = (const float*)(Ks + 16384);
-    if (active) {
-      bf16x8 kf[2][4];
+  // Pass 1: fixed reference 0 (Q carries log2(e)/8, so p = 2^s) -- no per-tile max, vote or rescale;
+  // valid while every row sum stays in [2^-60, 2^100) (then every p <= 2^100: fp32 and bf16 hold it).
+  // Otherwise the block re-runs with the lazily raised running max (pass 2, LAZY), as attention_pipe.hip does.
+  auto run_pass = [&](auto lazyc) __attribute__((always_inline)) {
+    constexpr bool LAZY = decltype(lazyc)::value;
+    f32x16 negm[NCH];  // (the re-run pass only: local, so the first pass holds no registers for them)
+    float mref[NCH];
+    bool have_m[NCH];  // mref set (a tile with an unmasked key seen)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+    for (int ch = 0; ch < NCH; ++ch) {
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) kf[u][ks] = *(const bf16x8*)(Ks + a64_off(32 * u + r, 2 * ks + hh));
-      f32x16 s[NCH][2];
-#pragma unroll
-      for (int ch = 0; ch < NCH; ++ch)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          s[ch][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qf[ch][0], negm, 0, 0, 0);
-#pragma unroll
-          for (int ks = 1; ks < 4; ++ks)
-            s[ch][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][ks], qf[ch][ks], s[ch][u], 0, 0, 0);
-        }
-      if (kbias != nullptr || (it == ntiles - 1 && (L % A64_KT) != 0)) {  // key bias and keys past L (0 / -inf)
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float bv = Bs[32 * u + (i & 3) + 8 * (i >> 2) + 4 * hh];
-#pragma unroll
-            for (int ch = 0; ch < NCH; ++ch)
-              s[ch][u][i] = bv == 0.f ? s[ch][u][i] : (bv == -INFINITY ? -INFINITY : s[ch][u][i] + bv * kLog2e);
-          }
-      }
-      float tm = -INFINITY;
-#pragma unroll
-      for (int ch = 0; ch < NCH; ++ch)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) tm = fmaxf(tm, fmaxf(s[ch][0][i], s[ch][1][i]));
-      {
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tm), __float_as_uint(tm), false, false);
-        tm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-      }
-      if (__any(!have_m || tm > A64_TAU)) {  // wave-uniform lazy rescale
-        const float delta = !have_m ? (tm == -INFINITY ? 0.f : tm) : fmaxf(tm, 0.f);
-        have_m = have_m || tm != -INFINITY;
-        const float alpha = exp2f(-delta);
-        mref += delta;
-#pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) o[ch][0][i] *= alpha, o[ch][1][i] *= alpha;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) lacc[ch][i] *= alpha;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            s[ch][0][i] -= delta;
-            s[ch][1][i] -= delta;
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) negm[i] = -mref;
-      }
-      // V^T A fragments (lane: d = 32 db + (lane & 31); elements j: keys b + (j & 3) + 8 (j >> 2), b = 16 ks + 4 hh,
-      // the P fragment's key order) as two transposed 4-key reads; lane 4q + p of each 16-lane group addresses
-      // key b + q (+ 8), d's 16 ((lane >> 4) & 1) + 4p .. +3 of its block (active is wave-uniform: EXEC is full)
-      bf16x8 vf[2][4];
-      {
-        const int q = (lane & 15) >> 2, p4 = lane & 3, dh = (lane >> 4) & 1;
-#pragma unroll
-        for (int db = 0; db < 2; ++db)
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            const int kb = 16 * ks + 4 * hh + q, cc = 4 * db + 2 * dh + (p4 >> 1);
-            const a64_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) a64_s4*)(Vs + a64v_off(kb, cc) + 8 * (p4 & 1)));
-            const a64_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) a64_s4*)(Vs + a64v_off(kb + 8, cc) + 8 * (p4 & 1)));
-            const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
-            vf[db][ks] = bf16x8{l4[0], l4[1], l4[2], l4[3], h4[0], h4[1], h4[2], h4[3]};
-          }
-      }
-      // chain by chain (a chain's scores die after its P.V): the next chain's exps issue beside this chain's MFMAs
-#pragma unroll
-      for (int ch = 0; ch < NCH; ++ch)
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int sp = 0; sp < 2; ++sp) {
-            bf16x8 pb;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) pb[j] = (bf16)__builtin_amdgcn_exp2f(s[ch][u][8 * sp + j]);
-            const int ks = 2 * u + sp;
-            o[ch][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0][ks], pb, o[ch][0], 0, 0, 0);
-            o[ch][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[1][ks], pb, o[ch][1], 0, 0, 0);
-            lacc[ch] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[ch], 0, 0, 0);
-          }
+      for (int i = 0; i < 16; ++i) negm[ch][i] = 0.f;
+      mref[ch] = 0.f;
+      have_m[ch] = false;
     }
-    if (it + 1 < ntiles) lstore((it + 1) & 1);
-    __syncthreads();
+    for (int it = 0; it < ntiles; ++it) {
+      const int k0 = it * A64_KT;
+      if (it + 1 < ntiles) gload(k0 + A64_KT);
+      const unsigned char* Ks = lds[it & 1];
+      const unsigned char* Vs = Ks + 8192;
+      const float* Bs = (const float*)(Ks + 16384);
+      if (active) {
+        bf16x8 kf[2][4];
+  #pragma unroll
+        for (int u = 0; u < 2; ++u)
+  #pragma unroll
+          for (int ks = 0; ks < 4; ++ks) kf[u][ks] = *(const bf16x8*)(Ks + a64_off(32 * u + r, 2 * ks + hh));
+        f32x16 s[NCH][2];
+  #pragma unroll
+        for (int ch = 0; ch < NCH; ++ch)
+  #pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            s[ch][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][0], qf[ch][0], LAZY ? negm[ch] : zero16, 0, 0,
+                                                               0);
+  #pragma unroll
+            for (int ks = 1; ks < 4; ++ks)
+              s[ch][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[u][ks], qf[ch][ks], s[ch][u], 0, 0, 0);
+          }
+        if (kbias != nullptr || (it == ntiles - 1 && (L % A64_KT) != 0)) {  // key bias and keys past L (0 / -inf)
+  #pragma unroll
+          for (int u = 0; u < 2; ++u)
+  #pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const float bv = Bs[32 * u + (i & 3) + 8 * (i >> 2) + 4 * hh];
+  #pragma unroll
+              for (int ch = 0; ch < NCH; ++ch)
+                s[ch][u][i] = bv == 0.f ? s[ch][u][i] : (bv == -INFINITY ? -INFINITY : s[ch][u][i] + bv * kLog2e);
+            }
+        }
+        if constexpr (LAZY) {
+    #pragma unroll
+          for (int ch = 0; ch < NCH; ++ch) {
+            float tm = fmaxf(s[ch][0][0], s[ch][1][0]);
+    #pragma unroll
+            for (int i = 1; i < 16; ++i) tm = fmaxf(tm, fmaxf(s[ch][0][i], s[ch][1][i]));
+            {
+              const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tm), __float_as_uint(tm), false, false);
+              tm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+            }
+            if (__any(!have_m[ch] || tm > A64_TAU)) {  // wave-uniform lazy rescale
+              const float delta = !have_m[ch] ? (tm == -INFINITY ? 0.f : tm) : fmaxf(tm, 0.f);
+              have_m[ch] = have_m[ch] || tm != -INFINITY;
+              const float alpha = exp2f(-delta);
+              // the row sums' selector output: lane l < 16 holds query l's sum (element 0) and query l + 16's
+              // (element 1; elements 2, 3 and lanes >= 16 are zero rows), so element 1 takes lane l + 16's factor
+              const float alpha16 = __shfl(alpha, (lane & 15) + 16, 64);
+              mref[ch] += delta;
+    #pragma unroll
+              for (int i = 0; i < 16; ++i) {
+                o[ch][0][i] *= alpha, o[ch][1][i] *= alpha;
+                s[ch][0][i] -= delta;
+                s[ch][1][i] -= delta;
+                negm[ch][i] = -mref[ch];
+              }
+              lacc[ch][0] *= alpha;
+              lacc[ch][1] *= alpha16;
+            }
+          }
+        }
+        // V^T A fragments (lane: d = 32 db + (lane & 31); elements j: keys b + (j & 3) + 8 (j >> 2), b = 16 ks + 4 hh,
+        // the P fragment's key order) as two transposed 4-key reads; lane 4q + p of each 16-lane group addresses
+        // key b + q (+ 8), d's 16 ((lane >> 4) & 1) + 4p .. +3 of its block (active is wave-uniform: EXEC is full)
+        bf16x8 vf[2][4];
+        {
+          const int q = (lane & 15) >> 2, p4 = lane & 3, dh = (lane >> 4) & 1;
+  #pragma unroll
+          for (int db = 0; db < 2; ++db)
+  #pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+              const int kb = 16 * ks + 4 * hh + q, cc = 4 * db + 2 * dh + (p4 >> 1);
+              const a64_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                  (__attribute__((address_space(3))) a64_s4*)(Vs + a64v_off(kb, cc) + 8 * (p4 & 1)));
+              const a64_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                  (__attribute__((address_space(3))) a64_s4*)(Vs + a64v_off(kb + 8, cc) + 8 * (p4 & 1)));
+              const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
+              vf[db][ks] = bf16x8{l4[0], l4[1], l4[2], l4[3], h4[0], h4[1], h4[2], h4[3]};
+            }
+        }
+        // chain by chain (a chain's scores die after its P.V): the next chain's exps issue beside this chain's MFMAs
+  #pragma unroll
+        for (int ch = 0; ch < NCH; ++ch)
+  #pragma unroll
+          for (int u = 0; u < 2; ++u)
+  #pragma unroll
+            for (int sp = 0; sp < 2; ++sp) {
+              bf16x8 pb;
+  #pragma unroll
+              for (int j = 0; j < 8; ++j) pb[j] = (bf16)__builtin_amdgcn_exp2f(s[ch][u][8 * sp + j]);
+              const int ks = 2 * u + sp;
+              o[ch][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0][ks], pb, o[ch][0], 0, 0, 0);
+              o[ch][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[1][ks], pb, o[ch][1], 0, 0, 0);
+              lacc[ch] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc[ch], 0, 0, 0);
+            }
+      }
+      if (it + 1 < ntiles) lstore((it + 1) & 1);
+      __syncthreads();
+    }
+  };
+  run_pass(std::false_type{});
+  {
+    bool bad = false;
+    if (active)
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const float la = __shfl(lacc[ch][0], lane & 15, 64), lb = __shfl(lacc[ch][1], lane & 15, 64);
+        const float ls = r < 16 ? la : lb;
+        bad |= !(ls >= 0x1p-60f && ls < 0x1p100f) && qi[ch] < nq;  // also 0 (underflow or every key masked), inf, NaN
+      }
+    if (__syncthreads_or(bad ? 1 : 0)) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[ch][0][i] = o[ch][1][i] = 0.f;
+        lacc[ch] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      gload(0);
+      lstore(0);
+      __syncthreads();
+      run_pass(std::true_type{});
+    }
   }
   if (!active) return;
 #pragma unroll

@@ -8,6 +8,8 @@ Tolerances (rel = max |d| / max(1, max |ref|)):
   case below, about twice the deviation measured on MI355X (printed by each test).
 """
 
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -142,3 +144,63 @@ def test_electra_out_of_range_ids_raise():
     m = text_model("electra_proj_masked")
     with pytest.raises(IndexError):
         m(torch.tensor([[1, 2, 5000]]).cuda())
+
+
+def _attn_ref(qkv, kbias, bf16_q=False):
+    """fp64 softmax attention of qkv [B][L][3][H][64] (values as given), key bias [B][L] or None.  bf16_q: the
+    bf16 kernel's own query operand, bf16(q * log2(e) / 8) with the scores in log2 units -- at large scores that
+    rounding (2^-9 of a score of a few hundred) moves the softmax more than anything the kernel does after it,
+    so the check holds the kernel to the arithmetic it is specified to do from there on."""
+    q, k, v = (qkv[:, :, i].double().transpose(1, 2) for i in range(3))  # [B][H][L][64]
+    if bf16_q:
+        c = torch.tensor(math.log2(math.e), dtype=torch.float32) * 0.125
+        q = (q.float() * c).bfloat16().double() / math.log2(math.e)  # natural units again for the softmax below
+    s = q @ k.transpose(-1, -2) / (1.0 if bf16_q else 8.0)
+    if kbias is not None:
+        s = s + kbias.double()[:, None, None, :]
+    return (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(qkv.shape[0], qkv.shape[1], -1)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "f32"])
+@pytest.mark.parametrize("case", ["plain", "large_scores", "masked_keys", "masked_row"])
+def test_attention_tap_matches_softmax(case, prec):
+    """mmpfn_enc_attention (the towers' attention kernel) against an fp64 softmax of the same inputs.  L = 577
+    (a partial last key tile); large_scores: q x 40 puts the row sums past 2^100, so the bf16 kernel's
+    fixed-reference pass gives way to its running-max re-run; masked_keys: -inf key bias on a third of the keys;
+    masked_row: every key of the second sequence excluded -> 0 (the kernel's defined output)."""
+    from multimodalpfn_amd import _lib
+
+    lib = _lib.load_library()
+    enc = lib.mmpfn_enc_create(0, None)
+    try:
+        B, L, H = 2, 577, 4
+        g = torch.Generator().manual_seed(7)
+        qkv = torch.randn(B, L, 3, H, 64, generator=g)
+        if case == "large_scores":
+            qkv[:, :, 0] *= 40.0
+        kb = None
+        if case in ("masked_keys", "masked_row"):
+            kb = torch.zeros(B, L)
+            kb[torch.rand(B, L, generator=g) < 1 / 3] = -float("inf")
+            kb[:, 0] = 0.0
+            if case == "masked_row":
+                kb[1] = -float("inf")
+        dt = torch.bfloat16 if prec == "bf16" else torch.float32
+        qd = qkv.to(dt).cuda()
+        kbd = kb.cuda() if kb is not None else None
+        out = torch.empty(B, L, H * 64, device="cuda", dtype=dt)
+        rc = lib.mmpfn_enc_attention(enc, qd.data_ptr(), kbd.data_ptr() if kbd is not None else None, out.data_ptr(),
+                                     B, L, H, 1 if prec == "bf16" else 0)
+        assert rc == 0, lib.mmpfn_enc_last_error(enc)
+        torch.cuda.synchronize()
+        got = out.float().cpu()
+        ref = _attn_ref(qd.float().cpu(), kb, bf16_q=prec == "bf16")
+        rows = [0] if case == "masked_row" else [0, 1]
+        err = rel(got[rows].numpy(), ref[rows].numpy())
+        print(f"attention tap {case} {prec}: {err:.3e}")
+        assert torch.isfinite(got).all()
+        assert err <= (1e-2 if prec == "bf16" else F32_TOL), err  # measured: bf16 1.6-2.6e-3, f32 4e-7 .. 1.4e-5
+        if case == "masked_row":
+            assert (got[1] == 0).all()
+    finally:
+        lib.mmpfn_enc_destroy(enc)
