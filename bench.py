@@ -10,8 +10,9 @@ One step = one ``predict_proba`` of the hot path on device-resident inputs: mixe
 (the image is identical for every member), 4 member forwards per GPU, one RCCL
 all-gather of the per-member logits, ensemble softmax-mean.  ``value`` = sum over
 members of (N + Q) / wall time, aggregated over all ranks (weak scaling: 4 members
-per GPU); nothing else runs in the timed region.  Launch with ``torchrun
---nproc-per-node N bench.py --gpus N`` for N > 1.
+per GPU); nothing else runs in the timed region.  ``python bench.py --gpus N`` starts N rank
+processes itself (``launch_ranks``: one per GPU, rendezvous on 127.0.0.1); ``torchrun --nproc-per-node N
+bench.py --gpus N`` works the same way (every rank checks WORLD_SIZE == --gpus).
 
 Also reported (each in its own pass, outside the headline's timed region):
 ``roofline`` of the dominant kernel (sample-axis attention, bf16 MFMA; algorithmic
@@ -67,6 +68,8 @@ def parse():
     p.add_argument("--api-steps", type=int, default=3, help="timed predict_proba calls of the API leg (0: skip)")
     p.add_argument("--no-kv-cache", dest="kv_cache", action="store_false", help="skip the fit_with_cache leg")
     p.add_argument("--no-config-d", dest="config_d", action="store_false", help="skip the config-D leg")
+    p.add_argument("--no-config-b", dest="config_b", action="store_false",
+                   help="skip the config-B leg (4096 x 100 tabular, fp16 and bf16)")
     p.add_argument("--no-config-e", dest="config_e", action="store_false",
                    help="skip the config-E leg (fp16 vs the fp8 P.V path)")
     p.add_argument("--no-modality", dest="modality", action="store_false",
@@ -364,8 +367,22 @@ def api_end_to_end(cfg, sd, x, y, image, n_estimators, prec_f32, steps, world, p
         eng = model.engine(clf.device_)
         prec = _lib_prec(prec_f32)
         img = torch.from_numpy(np.ascontiguousarray(image, dtype=np.float32)).to(eng.device)
+        # this rank's members only, dealt exactly as the predict deals them (inference._run_members ->
+        # parallel.member_shard: LPT over parallel.member_cost, keyed by geometry, in units of the engine's batch),
+        # so the subtraction below compares the same work
+        from multimodalpfn_amd.inference import _n_mixer_tokens
+        from multimodalpfn_amd.parallel import lpt_assign, member_cost
+
+        fpg = model.features_per_group
+        C = _n_mixer_tokens(model, imq)
+        keys = [(int(np.asarray(xt).shape[1]), len(yt)) for xt, yt in zip(ex.X_trains, ex.y_trains)]
+        costs = [member_cost((f + fpg - 1) // fpg + C + 1, len(yt) + len(Xq), len(yt), model.cfg.emsize, model.cfg.nhid)
+                 for (f, _), yt in zip(keys, ex.y_trains)]
+        mine = (lpt_assign(costs, world, keys, eng.batch)[dist.get_rank()] if world > 1
+                else list(range(len(ex.X_trains))))
         items = []
-        for xt, xq, yt in zip(ex.X_trains, Xts, ex.y_trains):
+        for i in mine:
+            xt, xq, yt = ex.X_trains[i], Xts[i], ex.y_trains[i]
             xf = torch.from_numpy(np.ascontiguousarray(np.concatenate([xt, xq], 0), dtype=np.float32)).to(eng.device)
             items.append((xf, np.asarray(yt, np.float32)))
 
@@ -381,7 +398,8 @@ def api_end_to_end(cfg, sd, x, y, image, n_estimators, prec_f32, steps, world, p
         torch.cuda.synchronize()
         t_dev = (time.perf_counter() - t0) / steps
         out["ragged_members_device"] = {
-            "value": round(n_estimators * S_ROWS / t_dev, 1), "unit": "rows/s", "ms_per_step": round(t_dev * 1e3, 3),
+            "value": round(len(items) * S_ROWS / t_dev, 1), "unit": "rows/s", "ms_per_step": round(t_dev * 1e3, 3),
+            "members_this_rank": len(items),
             "geometries": len({w for w in widths}),
             "note": "mixer + the default-preprocessing members (ragged widths) through forward_many on "
                     "device-resident inputs; equal-width members batch, ragged ones overlap on lanes",
@@ -493,15 +511,35 @@ def config_e_leg(device, args):
     4 members (feature shuffle + class permutation) through forward_many: the fp16 mode, and the same with the
     sample-axis attention's P.V on fp8 MFMA (MMPFN_PREC_F16_F8, config E's "fp8 MFMA path").  rows/s =
     members * (N + Q) / step time; every attention launch also timed by HIP events (mmpfn_kernel_timing)."""
+    from multimodalpfn_amd import _lib
+
+    return tabular_config_leg(
+        device, "config E: N=10000 support + Q=2000 query rows, F=20 tabular, 12 layers, 4 members",
+        12000, 10000, 20, 4, 4,
+        (("f16", _lib.PREC_F16), ("f16 + fp8 P.V (e4m3)", _lib.PREC_F16_F8),
+         ("f16 + fp8 P.V (e5m2)", _lib.PREC_F16_F8E5), ("bf16", _lib.PREC_BF16)))
+
+
+def config_b_leg(device, args):
+    """BASELINE config B: 4096 support + 1024 query rows x 100 features, tabular-only, 12 layers (SURVEY 8d seed 1;
+    T = 51 tokens per row, item attention ~72 % of the flops), 4 members through forward_many, fp16 and bf16."""
+    from multimodalpfn_amd import _lib
+
+    return tabular_config_leg(
+        device, "config B: N=4096 support + Q=1024 query rows, F=100 tabular, 12 layers, 4 members",
+        5120, 4096, 100, 2, 1, (("f16", _lib.PREC_F16), ("bf16", _lib.PREC_BF16)))
+
+
+def tabular_config_leg(device, workload, S, N, F, ncls, seed, modes, M=4):
+    """A tabular-only BASELINE config through forward_many, one record per precision mode (the first is the
+    reference point of the others' logits deviation)."""
     import ctypes
 
     from synth import synth_labels, synth_state_dict, synth_table
 
-    from multimodalpfn_amd import _lib
     from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
     from multimodalpfn_amd.model.transformer import PerFeatureTransformer
 
-    S, N, F, ncls, seed, M = 12000, 10000, 20, 4, 4, 4
     cfg = ModelConfig(mgm_heads=8, cap_heads=4)
     sd = synth_state_dict(state_dict_spec(cfg), seed)
     model = PerFeatureTransformer(cfg)
@@ -517,10 +555,10 @@ def config_e_leg(device, args):
     for _ in range(M):
         xm = torch.from_numpy(np.ascontiguousarray(x[:, rng.permutation(F)])).to(device)
         items.append((xm, None, rng.permutation(ncls)[y[:N].astype(np.int64)].astype(np.float32)))
-    out = {"workload": "config E: N=10000 support + Q=2000 query rows, F=20 tabular, 12 layers, 4 members"}
+    out = {"workload": workload}
     ref = None
-    for name, code in (("f16", _lib.PREC_F16), ("f16 + fp8 P.V (e4m3)", _lib.PREC_F16_F8),
-                       ("f16 + fp8 P.V (e5m2)", _lib.PREC_F16_F8E5), ("bf16", _lib.PREC_BF16)):
+    ref_name = modes[0][0]
+    for name, code in modes:
         def step():
             return eng.forward_many(items, code)
 
@@ -540,8 +578,8 @@ def config_e_leg(device, args):
             ref = lg
         else:
             d = (lg - ref).abs().max().item() / max(1.0, ref.abs().max().item())
-            rec["logits_rel_dev_vs_f16"] = float(f"{d:.3e}")
-            rec["argmax_agree_vs_f16"] = round(float((lg.argmax(-1) == ref.argmax(-1)).float().mean()), 4)
+            rec[f"logits_rel_dev_vs_{ref_name}"] = float(f"{d:.3e}")
+            rec[f"argmax_agree_vs_{ref_name}"] = round(float((lg.argmax(-1) == ref.argmax(-1)).float().mean()), 4)
         out[name] = rec
     eng.close()
     return out
@@ -607,9 +645,70 @@ def modality_leg(device, args):
     return out
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n: int, port: int, base: dict | None = None) -> list[dict]:
+    """The environment of each of the n rank processes ``launch_ranks`` starts on this node: torchrun's
+    variables (one process per GPU, LOCAL_RANK = RANK), the rendezvous on 127.0.0.1, dmabuf IPC for RCCL."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n: int, cmd: list[str], stdout=None, poll_s: float = 0.2) -> int:
+    """``bench.py --gpus N`` without torchrun: start N fresh rank processes running ``cmd`` (this script again,
+    with WORLD_SIZE set) and wait for them.  The parent never initialises HIP -- it only forks children, so
+    nothing is exec'd from a process that touched the GPU.  The first rank that fails ends the others; the
+    return value is 0 or that rank's exit status (128 + signal for a killed rank).  Rank 0 prints the JSON line
+    on the inherited stdout (the other ranks' stdout goes to stderr, so stdout carries one rank's output)."""
+    import subprocess
+
+    procs = [subprocess.Popen(cmd, env=e, stdout=stdout if r == 0 else sys.stderr)
+             for r, e in enumerate(rank_envs(n, free_port()))]
+    rc = 0
+    try:
+        pending = set(range(n))
+        while pending:
+            for i in sorted(pending):
+                r = procs[i].poll()
+                if r is None:
+                    continue
+                pending.discard(i)
+                if r != 0 and rc == 0:
+                    rc = r if r > 0 else 128 - r
+                    print(f"bench launcher: rank {i} exited with {r}; stopping the other ranks", file=sys.stderr)
+                    for p in procs:
+                        if p.poll() is None:
+                            p.terminate()
+            if pending:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # plain `python bench.py --gpus N`: become the launcher of N rank processes (torchrun's job)
+        sys.exit(launch_ranks(args.gpus, [sys.executable, "-u", str(Path(__file__).resolve()), *sys.argv[1:]]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the world must be one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -750,6 +849,12 @@ def main():
                     k: r[k] for k in ("achieved", "frac", "per_launch_ms")}
     eng.close()
     cfg_d = config_d_leg(device, world, rank, args, prec) if args.config_d else None
+    cfg_b = None
+    if args.config_b and rank == 0:
+        try:
+            cfg_b = config_b_leg(device, args)
+        except Exception as e:  # noqa: BLE001 - reported, the headline number stands on its own
+            cfg_b = {"error": f"{type(e).__name__}: {e}"}
     cfg_e = None
     if args.config_e and rank == 0:
         try:
@@ -815,6 +920,7 @@ def main():
             "api_end_to_end_default_preprocessing": api_def,
             "other_16bit_mode": other16,
             "f32_parity_mode": f32,
+            "config_B": cfg_b,
             "config_D": cfg_d,
             "config_E": cfg_e,
             "kv_cache_predict": kv,

@@ -494,6 +494,11 @@ GemmArgs gargs() {
     if (rc_ != MMPFN_OK) return rc_; \
   } while (0)
 
+// whether PREC_F16's layer kernels take this model / table: E = 192 in 6 heads and at most 64 tokens per row
+// (T < 0: a row-wise sublayer, no token limit).  Everything else runs PREC_BF16 -- the forward (embed) and the
+// per-sublayer taps (state_tap) apply the same rule.
+inline bool f16_fits(const mmpfn_model_desc& d, int T) { return d.emsize == 192 && d.nhead == 6 && T <= 64; }
+
 // member m (of M, all of the geometry set by member 0) -> X[m] = embedded input [T][S][E]
 int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int C, const float* y, int N,
           const float* uniq, int U, const float* pos_rand, int prec, int m = 0, int M = 1) {
@@ -509,7 +514,7 @@ int embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int
   const int G = x ? (F + fpg - 1) / fpg : 0;
   const int T = G + C + 1;
   // PREC_F16's layer kernels hold a row's tokens as up to four 16-token tiles; wider tables run PREC_BF16
-  if (prec == PREC_F16 && (T > 64 || E != 192 || d.nhead != 6)) prec = PREC_BF16;
+  if (prec == PREC_F16 && !f16_fits(d, T)) prec = PREC_BF16;
   const int Npad = (N + 63) / 64 * 64;
   const size_t R = (size_t)S * T;
   hipStream_t st = ctx->stream;
@@ -989,11 +994,12 @@ int mixer(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, i
 }
 
 // a tap on the caller's fp32 state: PREC_F16 runs it on an fp16 copy and converts the result back
-// (f16_ok false: the sublayer has no fp16 form at this shape and runs PREC_BF16, as the forward does)
+// (T: the state's tokens per row, -1 for a row-wise sublayer; where f16_fits says no, the sublayer runs PREC_BF16,
+// as the forward does)
 template <typename F>
-int state_tap(mmpfn_ctx* ctx, float* X, int64_t n, int precision, bool f16_ok, F&& run) {
+int state_tap(mmpfn_ctx* ctx, float* X, int64_t n, int precision, int T, F&& run) {
   int bp = base_prec(precision);
-  if (bp == PREC_F16 && !f16_ok) bp = PREC_BF16;
+  if (bp == PREC_F16 && !f16_fits(ctx->d, T)) bp = PREC_BF16;
   if (bp != PREC_F16) return run((void*)X, bp);
   RC(ensure(ctx, ctx->tap_x16, (size_t)n * 2));
   HIPCHK(launch_f32_to_f16(X, 0, ctx->tap_x16.p, 0, n, 1, ctx->stream));
@@ -1230,8 +1236,12 @@ int mmpfn_item_attention(mmpfn_ctx* ctx, const void* q, const void* k, const voi
   if (s0 < 0 || nq < 0 || s0 + nq > S || nk <= 0 || nk > Npad || Npad % 64 || H <= 0 || T <= 0 || kvh >= H)
     return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
   HIPCHK(hipSetDevice(ctx->device));
-  if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
-  HIPCHK(launch_attn_item(q, k, vt, out, S, T, H, Npad, s0, nq, nk, kvh, base_prec(precision), ctx->stream));
+  // this entry point runs the bf16 and the two fp32 element forms only (launch_attn_item); fp16 Q / K and the
+  // fp8 P.V variants go through mmpfn_item_attention_layer_ex
+  if (precision != PREC_F32 && precision != PREC_BF16 && precision != PREC_F32_MFMA)
+    return fail(ctx, MMPFN_ERR_INVALID, "bad precision (PREC_F32, PREC_BF16 or PREC_F32_MFMA; 16-bit / fp8 Q.K forms: "
+                                        "mmpfn_item_attention_layer_ex)");
+  HIPCHK(launch_attn_item(q, k, vt, out, S, T, H, Npad, s0, nq, nk, kvh, precision, ctx->stream));
   return MMPFN_OK;
 }
 
@@ -1386,7 +1396,7 @@ int mmpfn_feature_attention(mmpfn_ctx* ctx, int layer, float* X, int S, int T, i
   RC(tap_check(ctx, layer, X, precision));
   if (S <= 0 || T <= 0) return fail(ctx, MMPFN_ERR_INVALID, "bad state geometry");
   RC(tap_workspace(ctx, S, T, 64));
-  return state_tap(ctx, X, (int64_t)S * T * ctx->d.emsize, precision, T <= 64, [&](void* Xs, int bp) {
+  return state_tap(ctx, X, (int64_t)S * T * ctx->d.emsize, precision, T, [&](void* Xs, int bp) {
     return feat_sublayer(ctx, ctx->layers[layer], Xs, S, T, 1, bp);
   });
 }
@@ -1396,7 +1406,7 @@ int mmpfn_item_attention_block(mmpfn_ctx* ctx, int layer, float* X, int S, int T
   if (S <= 0 || T <= 0 || N <= 0 || N > S) return fail(ctx, MMPFN_ERR_INVALID, "bad state geometry");
   const int Npad = (N + 63) / 64 * 64;
   RC(tap_workspace(ctx, S, T, Npad));
-  return state_tap(ctx, X, (int64_t)S * T * ctx->d.emsize, precision, true, [&](void* Xs, int bp) {
+  return state_tap(ctx, X, (int64_t)S * T * ctx->d.emsize, precision, T, [&](void* Xs, int bp) {
     return item_sublayer(ctx, layer, Xs, S, T, N, Npad, 1, bp, false, f8_of(precision));
   });
 }
@@ -1404,7 +1414,7 @@ int mmpfn_item_attention_block(mmpfn_ctx* ctx, int layer, float* X, int S, int T
 int mmpfn_mlp_ln(mmpfn_ctx* ctx, int layer, float* X, int64_t rows, int precision) {
   RC(tap_check(ctx, layer, X, precision));
   if (rows <= 0) return fail(ctx, MMPFN_ERR_INVALID, "bad row count");
-  return state_tap(ctx, X, rows * ctx->d.emsize, precision, true, [&](void* Xs, int bp) {
+  return state_tap(ctx, X, rows * ctx->d.emsize, precision, -1, [&](void* Xs, int bp) {
     return mlp_sublayer(ctx, ctx->layers[layer], Xs, rows, bp, nullptr);
   });
 }

@@ -631,3 +631,70 @@ def test_mixer_bf16_matches_fp32(mixer, mgm, cap, S):
     assert torch.isfinite(got).all()
     err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
     assert err < 3e-2, err
+
+
+def test_item_attention_entry_rejects_16bit_and_fp8_codes():
+    """``mmpfn_item_attention`` runs the bf16 and the two fp32 element forms only: the fp16 Q / K and
+    fp8 P.V codes 3-7 belong to ``mmpfn_item_attention_layer_ex`` and must be refused, not run on the fp32 kernel."""
+    from multimodalpfn_amd import _lib
+    from multimodalpfn_amd.engine import HipEngine  # noqa: F401
+
+    lib = _lib.load_library()
+    ctx = lib.mmpfn_create(0, None)
+    S, N, T, H, d, Npad = 70, 40, 1, 6, 32, 64
+    q = torch.zeros(T, H, S, d, device="cuda", dtype=torch.float32)
+    k = torch.zeros(T, H, Npad, d, device="cuda", dtype=torch.float32)
+    vt = torch.zeros(T, H, d, Npad, device="cuda", dtype=torch.float32)
+    out = torch.full((T, S, H * d), 7.0, device="cuda", dtype=torch.float32)
+    try:
+        for code in (3, 4, 5, 6, 7, 8, -1):
+            rc = lib.mmpfn_item_attention(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), out.data_ptr(), S, T, H,
+                                          Npad, 0, N, N, -1, code)
+            assert rc == _lib.MMPFN_ERR_INVALID, (code, rc)
+        torch.cuda.synchronize()
+        assert (out == 7.0).all()  # nothing ran
+        assert lib.mmpfn_item_attention(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), out.data_ptr(), S, T, H,
+                                        Npad, 0, N, N, -1, _lib.PREC_F32) == 0
+        torch.cuda.synchronize()
+    finally:
+        lib.mmpfn_destroy(ctx)
+
+
+@pytest.mark.parametrize("emsize,nhead,F", [(192, 6, 140), (128, 4, 9)])
+def test_f16_falls_back_to_bf16_outside_its_kernels(emsize, nhead, F):
+    """PREC_F16's layer kernels take E = 192 in 6 heads and at most 64 tokens per row; anything else runs the bf16
+    mode.  The forward, the train-KV cache and every sublayer tap apply the same rule, so PREC_F16 equals
+    PREC_BF16 bitwise there: 140 features (71 tokens per row) and a 128-wide, 4-head model."""
+    from synth import synth_labels, synth_state_dict, synth_table
+
+    from multimodalpfn_amd import _lib
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    cfg = ModelConfig(nlayers=2, emsize=emsize, nhead=nhead, mgm_heads=8, cap_heads=4)
+    sd = synth_state_dict(state_dict_spec(cfg), 21)
+    model = make_model(cfg, sd)
+    eng = model.engine()
+    S, N = 260, 200
+    x = torch.from_numpy(synth_table(S, F, 21, n_cat=2)).cuda()
+    y = synth_labels(S, 3, 21)[:N]
+    with torch.inference_mode():
+        h = eng.forward(x, None, y, _lib.PREC_F16)
+        b = eng.forward(x, None, y, _lib.PREC_BF16)
+        eng.status()
+        assert torch.isfinite(h).all()
+        assert torch.equal(h, b)
+        ch, cb = eng.cache_build(x[:N], None, y, _lib.PREC_F16), eng.cache_build(x[:N], None, y, _lib.PREC_BF16)
+        ph, pb = eng.cache_predict(ch, x[N:], None), eng.cache_predict(cb, x[N:], None)
+        ch.free()
+        cb.free()
+        assert torch.equal(ph, pb)
+        assert torch.equal(ph, h)
+        X = eng.embed_state(x, None, y, _lib.PREC_F32)
+        T = X.shape[1]
+        if emsize == 192:
+            assert T > 64
+            assert torch.equal(eng.feature_attention(0, X, _lib.PREC_F16), eng.feature_attention(0, X, _lib.PREC_BF16))
+        else:
+            assert torch.equal(eng.item_attention_block(0, X, N, _lib.PREC_F16),
+                               eng.item_attention_block(0, X, N, _lib.PREC_BF16))
+            assert torch.equal(eng.mlp_ln(0, X, _lib.PREC_F16), eng.mlp_ln(0, X, _lib.PREC_BF16))
