@@ -51,14 +51,19 @@ typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(2))) short s16x2;
 
-// fp8 P formats: conversion, MFMA operand format code, where the first tile's max lands (2^ETOP) and the
-// smallest power of two the format still holds (subnormal)
+// fp8 P formats: conversion, MFMA operand format code, where the first tile's max lands (2^ETOP), the
+// smallest power of two the format still holds (subnormal) and the underflow guard UFLOW = 2^(EMIN + 6): a
+// scaled P' below 2^(EMIN-1) converts to 0 and every subnormal is off by at most that much, so a row's fp8 sum
+// L is within nk 2^(EMIN-1) of the sum it stands for; L < nk UFLOW (more than 2^-7 of it possibly lost to the
+// format's floor: one large key in the first tile over many keys ~10 octaves below) re-runs the
+// wave on the exact bf16 path like an overflow does
 template <int F8> struct P8;
 #ifndef P8_E4_ETOP
 #define P8_E4_ETOP 0
 #endif
 template <> struct P8<1> {  // e4m3 (max 448 = 2^8.8): >= 7.8 octaves of headroom, 9 below the first max
   static constexpr int FMT = 0, ETOP = P8_E4_ETOP, EMIN = -9, EMAX = 8;
+  static constexpr float UFLOW = 0x1p-3f;
   static __device__ __forceinline__ s16x2 cvt(s16x2 old, float a, float b, float sc, bool hi) {
     return hi ? __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(old, a, b, sc, true)
               : __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(old, a, b, sc, false);
@@ -66,6 +71,7 @@ template <> struct P8<1> {  // e4m3 (max 448 = 2^8.8): >= 7.8 octaves of headroo
 };
 template <> struct P8<2> {  // e5m2 (max 57344 = 2^15.8): >= 8.8 octaves of headroom, 22 below
   static constexpr int FMT = 1, ETOP = 6, EMIN = -16, EMAX = 15;
+  static constexpr float UFLOW = 0x1p-10f;
   static __device__ __forceinline__ s16x2 cvt(s16x2 old, float a, float b, float sc, bool hi) {
     return hi ? __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(old, a, b, sc, true)
               : __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(old, a, b, sc, false);
@@ -645,6 +651,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       const unsigned lb = __float_as_uint(rs) & 0x7fffffffu;
       // (F8: the padded keys' ones are P'(0) each; a score past the format's range is NaN / inf here)
       bad |= lb >= 0x71800000u || lb < 0x21800000u || rs < padsum * padv[qb] * 0x1p-12f;
+      if constexpr (F8 != 0) bad |= rs < (float)p.nk * P8<F8>::UFLOW;  // the format's floor (UFLOW above)
     }
     if (__any(bad)) {
       zero_acc();

@@ -48,3 +48,25 @@ def test_oracle_sdpa_branch_agrees():
     a = oracle_forward(*args).numpy()
     b = oracle_forward(*args, use_sdpa=True).numpy()
     assert rel_err(a, b) < 1e-5
+
+
+def test_oracle_matches_reference_at_config_c_model():
+    """Config C's model (12 layers, MGM 64 + CAP 24, F = 21 with 18 categorical) on 600 rows: the oracle against
+    the reference's fp32 logits stored by make_f16_golden.py (pad_ufes_c_reduced)."""
+    import json
+
+    from synth import synth_state_dict
+
+    from helpers import GOLDEN
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    f = np.load(GOLDEN / "f16" / "pad_ufes_c_reduced.npz")
+    meta = json.loads(str(f["meta"]))
+    cfg = ModelConfig(**meta["cfg"])
+    sd = synth_state_dict(state_dict_spec(cfg), meta["wseed"])
+    out = oracle_forward(oracle_spec(cfg), torch_sd(sd), torch.from_numpy(f["x"]), torch.from_numpy(f["image"]),
+                         torch.from_numpy(f["y_train"])).numpy()
+    assert rel_err(out, f["logits_f32"]) < 1e-5
+    assert (out.argmax(1) == f["logits_f32"].argmax(1)).all()
+    # the reference's own fp16 autocast stays within a few 1e-3 of its fp32 forward (the fp16 mode's band)
+    assert rel_err(f["logits_f16"], f["logits_f32"]) < 5e-3
