@@ -312,45 +312,49 @@ def _f8_layer_ref(q, k, v, N, prec):
     return torch.cat([tr, te], 2).permute(0, 2, 1, 3).reshape(T, S, H * d)
 
 
+def _f8_outcomes(got, q, k, v, N, prec):
+    """Each (row, head) of an fp8 launch is one of two outcomes: the wave kept its fp8 pass (the quantising
+    reference) or re-ran on the exact bf16 path (an overflow past the format, or the underflow guard).  Returns the
+    per-(row, head) error against the nearer outcome and the fraction that re-ran."""
+    T, H, S, d = q.shape
+    got = got.double()
+    e_q = (got - _f8_layer_ref(q, k, v, N, prec)).reshape(T, S, H, d).abs().amax(-1)
+    e_x = (got - _layer_ref(q, k, v, N, 5 if prec >= 5 else 1)).reshape(T, S, H, d).abs().amax(-1)
+    return torch.minimum(e_q, e_x), (e_x < e_q).double().mean().item()
+
+
 @pytest.mark.parametrize("prec", [3, 4, 6, 7])
 @pytest.mark.parametrize("S,N,T", [(2298, 1838, 2), (70, 1, 2), (130, 64, 1), (200, 65, 3), (700, 333, 1),
                                    (12000, 10000, 1)])
 def test_item_attention_layer_fp8(S, N, T, prec):
     """Config E's fp8 path (MMPFN_PREC_{BF16,F16}_F8 / _F8E5): P.V and the row sums on block-scaled fp8 MFMA, the
     per-query scale from the first key tile, the partial tile's padded keys cancelled at P'(0) -- against a
-    reference that quantises V^T and P exactly as the kernel does (VERDICT r04 weak #7), within 1e-2 max|V|."""
+    reference that quantises V^T and P exactly as the kernel does, within 1e-2 max|V|; a wave
+    whose fp8 row sums fail the overflow / underflow checks re-runs exactly (small N: L < nk 2^(EMIN+6) often)."""
     q, k, v, Npad = _qkv_case(S, N, T, seed=S + N + prec)
     got = _launch_layer(q, k, v, Npad, N, prec)
-    ref = _f8_layer_ref(q, k, v, N, prec)
     assert torch.isfinite(got).all()
-    err = (got.double() - ref).abs().max().item()
-    rms = ((got.double() - ref) ** 2).mean().sqrt().item()
+    err, rerun = _f8_outcomes(got, q, k, v, N, prec)
     vmax = v.abs().max().item()
-    print(f"attention fp8 prec {prec} S={S} N={N} T={T}: max {err:.3e} rms {rms:.3e} (max|V| {vmax:.2f})")
-    assert err < F8_QBAND * vmax
+    print(f"attention fp8 prec {prec} S={S} N={N} T={T}: max {err.max():.3e} (max|V| {vmax:.2f}), re-run {rerun:.3f}")
+    assert err.max().item() < F8_QBAND * vmax
+    if N >= 1838:  # the fp8 pass itself is what runs at the configs' sizes
+        assert rerun < 0.5
 
 
 @pytest.mark.parametrize("prec", [3, 4, 6, 7])
 def test_item_attention_fp8_wide_score_spread(prec):
-    """Scores spread wide (the ATT_SCALE = 2 situation of DESIGN 5.5, here x3): later key tiles overflow the first
-    tile's fp8 scale for some queries, whose waves re-run on the exact bf16 path.  Every output row must be one of
-    the two outcomes -- the quantised fp8 result or the exact softmax -- and the re-run must have happened."""
+    """Scores spread wide (the ATT_SCALE = 2 situation of DESIGN 5.5, here x5): later key tiles overflow the first
+    tile's fp8 scale for some queries, whose waves re-run on the exact bf16 path.  Every output (row, head) must be
+    one of the two outcomes -- the quantised fp8 result or the exact softmax -- and the re-run must have happened."""
     S, N, T = 1200, 1000, 2
     q, k, v, Npad = _qkv_case(S, N, T, seed=77 + prec)
     q = q * 5.0
-    H = q.shape[1]
-    got = _launch_layer(q, k, v, Npad, N, prec).double()
-    qref = _f8_layer_ref(q, k, v, N, prec)
-    exact = _layer_ref(q, k, v, N, 5 if prec >= 5 else 1)
-    vmax = v.abs().max().item()
-    # per (row, head): a query's 32 outputs come from one wave, which either kept its fp8 pass or re-ran
-    e_q = (got - qref).reshape(T, S, H, -1).abs().amax(-1)
-    e_x = (got - exact).reshape(T, S, H, -1).abs().amax(-1)
-    ok = torch.minimum(e_q, e_x) < F8_QBAND * vmax
-    rerun = (e_x < e_q).double().mean().item()
-    print(f"wide spread prec {prec}: rows closer to the exact path {rerun:.3f}, worst {torch.minimum(e_q, e_x).max():.3e}")
+    got = _launch_layer(q, k, v, Npad, N, prec)
     assert torch.isfinite(got).all()
-    assert ok.all(), torch.minimum(e_q, e_x).max().item()
+    err, rerun = _f8_outcomes(got, q, k, v, N, prec)
+    print(f"wide spread prec {prec}: (row, head)s closer to the exact path {rerun:.3f}, worst {err.max():.3e}")
+    assert err.max().item() < F8_QBAND * v.abs().max().item()
     assert rerun > 0.0
 
 
