@@ -8,6 +8,6 @@ for v in "$@"; do
   cd /tmp || exit 1
   MMPFN_DIAGNOSTICS=1 MMPFN_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/kp_$v -o run --output-format csv -- \
     python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-modality --no-f32 --no-config-d --api-steps 0 \
-    --no-kv-cache --no-config-e --lanes 1 --batch 2 --attn-reps 2 > $R/gpurun_out/kp_$v.json 2> $R/gpurun_out/kp_$v.err || exit 1
+    --no-kv-cache --no-config-e --no-config-b --lanes 1 --batch 2 --attn-reps 2 > $R/gpurun_out/kp_$v.json 2> $R/gpurun_out/kp_$v.err || exit 1
   cd $R && echo "== $v" && python3 tools/ktrace_grid.py gpurun_out/kp_$v/run_kernel_trace.csv 12 || exit 1
 done

@@ -5,6 +5,6 @@
 set -o pipefail
 R=$PWD; O=$R/gpurun_out/rehearse; mkdir -p $O
 MMPFN_BENCH_SHARE_GPUS=1 MMPFN_BENCH_BACKEND=gloo timeout -k 10 500 python -u bench.py --gpus 2 --steps 3 --warmup 1 \
-  --no-cpu-baseline --no-modality --no-f32 --no-config-b --no-config-e --attn-reps 2 --api-steps 1 \
+  --no-cpu-baseline --no-modality --no-f32 --no-config-b --no-config-e --no-config-b --attn-reps 2 --api-steps 1 \
   > $O/bench2.json 2> $O/bench2.err || { tail -30 $O/bench2.err; exit 1; }
 tail -n 1 $O/bench2.json | head -c 1500
