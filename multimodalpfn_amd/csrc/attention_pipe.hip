@@ -254,8 +254,16 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   const int kso = krow * 32 + kc * 8, vso = vd * p.Npad + vc * 8;  // 32-bit lane offsets on wave-uniform bases
   const int kw = krow * KROW + 16 * kc;
   const int vw = F8 ? VBASE + vd * VROW + 32 * (vc & 1) + 8 * (vc >> 1) : VBASE + vd * VROW + 16 * vc;
-  u32x4 rk;
-  VStage rv;
+  // staging registers: P4_LEAD = 1: one set, tile t+3 loaded in step t and written to LDS in step t+1;
+  // P4_LEAD = 2: two sets (tile j in set j & 1), tile t+4 loaded in step t, written in step t+2, so a load has
+  // two steps to land instead of one (ablation: the K / V^T global loads cost ~40 us of a 258 us launch)
+#ifndef P4_LEAD
+#define P4_LEAD 2
+#endif
+  constexpr int LEAD = P4_LEAD;
+  static_assert(LEAD == 1 || LEAD == 2, "staging lead");
+  u32x4 rk[LEAD];
+  VStage rv[LEAD];
   auto gload = [&](int t, u32x4& k, VStage& v) __attribute__((always_inline)) {
     k = *(const u32x4*)(Kg + (int64_t)t * (P4_KT * 32) + kso);
     if constexpr (F8 != 0) v = *(const u32x2*)(Vg8 + t * P4_KT + vso);
@@ -486,22 +494,28 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     {  // tiles 0 and 1 in flight together, then tile 2 into the staging registers
       u32x4 rk1;
       VStage rv1;
-      gload(tile_of(0), rk, rv);
+      gload(tile_of(0), rk[0], rv[0]);
       gload(tile_of(min(1, ntiles - 1)), rk1, rv1);
-      if (partial) mask_pad(rk, rv);
-      lstore(ring, rk, rv);
+      if (partial) mask_pad(rk[0], rv[0]);
+      lstore(ring, rk[0], rv[0]);
       lstore(ring + P4_SLOT_BYTES, rk1, rv1);
     }
-    gload(tile_of(min(2, ntiles - 1)), rk, rv);
+    gload(tile_of(min(2, ntiles - 1)), rk[0], rv[0]);
+    if constexpr (LEAD == 2) gload(tile_of(min(3, ntiles - 1)), rk[1], rv[1]);
     lds_barrier();
     if (!active) {
       // a wave without queries (a kv sequence's last, partial task) stages its share of every tile and
       // meets every barrier, but issues none of the loop's MFMAs / exps: they would take issue slots
       // from the other block's wave on its SIMD
-      for (int t = 0; t < ntiles; ++t) {
-        lstore(ring + ((t + 2) & 3) * P4_SLOT_BYTES, rk, rv);
-        gload(tile_of(min(t + 3, ntiles - 1)), rk, rv);
+      for (int t = 0; t < ntiles; t += LEAD) {
+        lstore(ring + ((t + 2) & 3) * P4_SLOT_BYTES, rk[0], rv[0]);
+        gload(tile_of(min(t + 2 + LEAD, ntiles - 1)), rk[0], rv[0]);
         lds_barrier();
+        if (LEAD == 2 && t + 1 < ntiles) {
+          lstore(ring + ((t + 3) & 3) * P4_SLOT_BYTES, rk[LEAD - 1], rv[LEAD - 1]);
+          gload(tile_of(min(t + 5, ntiles - 1)), rk[LEAD - 1], rv[LEAD - 1]);
+          lds_barrier();
+        }
       }
       return;  // no barrier follows the fast pass
     }
@@ -555,8 +569,9 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       constexpr int S0 = L * P4_SLOT_BYTES, S1 = ((L + 1) & 3) * P4_SLOT_BYTES, S2 = ((L + 2) & 3) * P4_SLOT_BYTES;
       readk(kf[B], ring + S1);
       readv(vf[B], ring + S0);
-      lstore(ring + S2, rk, rv);
-      gload(tile_of(min(t + 3, ntiles - 1)), rk, rv);
+      constexpr int RS = LEAD == 2 ? A : 0;  // staging set of tile t+2 (and of t+2+LEAD, loaded next)
+      lstore(ring + S2, rk[RS], rv[RS]);
+      gload(tile_of(min(t + 2 + LEAD, ntiles - 1)), rk[RS], rv[RS]);
       smm(sb, kf[A], 1);
       expc(pa, sa, 0);
       pv(1, pz, vf[A]);
