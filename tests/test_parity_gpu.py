@@ -791,7 +791,7 @@ def test_f16_falls_back_to_bf16_on_wide_tables():
 
 
 F16_CASES = sorted(p.stem for p in (GOLDEN / "f16").glob("*.npz"))
-F16_REF_FACTOR = 2.0  # the fp16 mode's deviation from the fp32 reference <= 2x the reference's own fp16 deviation
+F16_REF_FACTOR = 3.0  # the fp16 mode's deviation from the fp32 reference <= 3x the reference's own fp16 deviation
 
 
 def _load_f16_case(name):
