@@ -8,15 +8,17 @@
 //   xf[ks]     X^T fragments of its 16 tokens (lane (n, g): X[token n][32ks + 8g .. +7]), loaded once, also
 //              the residual (the out-projection image's rows are in f16_row_perm order)
 //   per head   Q^T / K^T tiles = W_{q,k} . X^T on featrow's permuted weight rows (lane: Q[token n][8g .. +7]),
-//              V tile = X . Wv^T (lane: V[token 4g + i][d 16f + n]); its K fragment and V pieces go to LDS,
-//              one barrier, then its query tile attends to the row's NT key tiles read back from LDS -- in
+//              V tile = X . Wv^T (lane: V[token 4g + i][d 16f + n]); its K fragment and V pieces go to LDS, and
+//              after the next barrier its query tile attends to the row's NT key tiles read back from LDS -- in
 //              exactly the lane layout their producer computed them (K: the A operand of S^T = K Q^T, V: the
-//              halves of the A operand V^T of O^T = V^T P^T), so the exchange is lane-linear and conflict-free
+//              halves of the A operand V^T of O^T = V^T P^T), so the exchange is lane-linear and conflict-free;
+//              heads are software-pipelined (head h's attention beside head h+1's projections, one barrier per
+//              head: a first form with two barriers per head ran 116.8 vs featrow's 100.4 us)
 //   of[h]      the tile's O^T fragments of every head (6 x 4 VGPRs), out-projection after the last head
 //   y[f]       Y^T = Wout . O^T for its 16 tokens (12 tiles), then residual + LayerNorm across the 4 lane groups
 // ~150 VGPRs: three waves per SIMD with no spills.  Weights as in featrow.hip (the same LDS images, FR_ST-wide
-// rows, by LDS-DMA): per head a 39 KB QKV image double-buffered, the next head's in flight during the current
-// head, the 78 KB out-projection image over both buffers at the end; K / V exchange double-buffered by head
+// rows, by LDS-DMA): per head a 39 KB QKV image double-buffered, two heads ahead of its attention, the 78 KB
+// out-projection image over both buffers at the end; K / V exchange double-buffered by head
 // parity (4 NT KB per row).  MFMA work per row is featrow's; the lane arithmetic of every value is featrow's
 // too, so the two kernels agree bitwise.
 #include "common.h"
@@ -80,7 +82,7 @@ __global__ __launch_bounds__(64 * NT * FtRows<NT>::R, 1) void feat_tiles_kernel(
       __builtin_amdgcn_global_load_lds((const uint16_t*)src + p * 512 + lane * 8, (lds_void*)((uint16_t*)dst + p * 512),
                                        16, 0, 0);
   };
-  dma(pack, wbuf, FT_PIECES);  // head 0 -> buffer 0
+  dma(pack, wbuf, FT_PIECES);  // head 0 -> buffer 0 (head 1 -> buffer 1 after the first barrier)
   // ---- the tile's tokens (padding tokens t >= T are zero)
   const int t = 16 * tt + n;
   const bool pad = t >= T;
@@ -96,16 +98,12 @@ __global__ __launch_bounds__(64 * NT * FtRows<NT>::R, 1) void feat_tiles_kernel(
   __syncthreads();  // (its vmcnt(0) retires the DMA too)
 
   constexpr int NKP = (NT + 1) / 2;  // key-tile pairs (K = 32 keys per P.V MFMA)
-  f16x8 of[FT_H];
-#pragma unroll
-  for (int h = 0; h < FT_H; ++h) {
-    // the next image: head h+1's QKV, or after the last head the out-projection image's first half
-    dma(h + 1 < FT_H ? pack + (h + 1) * FT_QKV_IMG : pack + FT_H * FT_QKV_IMG,
-        h + 1 < FT_H ? wbuf + ((h + 1) & 1) * FT_QKV_IMG : wbuf, FT_PIECES);
+  f16x8 of[FT_H];                    // the tile's O^T fragments of every head
+  // ---- projections of head h (weights in wbuf[h & 1]): Q^T then K^T (C^T tiles) and V (C tile), K = 192 in
+  //      6 steps; Q stays in registers, the K fragment and the V pieces go to the exchange buffer of parity h & 1
+  auto project = [&](int h, f16x8& qf) __attribute__((always_inline)) {
     const f16* wq = wbuf + (h & 1) * FT_QKV_IMG;  // [96][FT_ST]: Q (permuted) | K (permuted) | V
-    unsigned char* kx = kvx + (h & 1) * KVS + rl * 2 * KVB;  // this row's K | V exchange
-    // ---- Q^T then K^T of the tile (C^T tiles), K = 192 in 6 steps
-    f16x8 qf;
+    unsigned char* kx = kvx + (h & 1) * KVS + rl * 2 * KVB;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       f32x4 qa[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -117,19 +115,19 @@ __global__ __launch_bounds__(64 * NT * FtRows<NT>::R, 1) void feat_tiles_kernel(
       if (j == 0) qf = cat8h(qa[0], qa[1]);
       else *(f16x8*)(kx + tt * 1024 + lane * 16) = cat8h(qa[0], qa[1]);  // K fragment of key tile tt
     }
-    {  // ---- V (C tile: lane = head dim, 4 consecutive tokens) -> its two halves of the V^T A operand
-      f32x4 va[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 va[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int ks = 0; ks < FT_E / 32; ++ks)
+    for (int ks = 0; ks < FT_E / 32; ++ks)
 #pragma unroll
-        for (int f = 0; f < 2; ++f)
-          va[f] = mfma16x(xf[ks], *(const f16x8*)(wq + (64 + 16 * f + n) * FT_ST + 32 * ks + 8 * g), va[f]);
+      for (int f = 0; f < 2; ++f)
+        va[f] = mfma16x(xf[ks], *(const f16x8*)(wq + (64 + 16 * f + n) * FT_ST + 32 * ks + 8 * g), va[f]);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) *(f16x4*)(kx + KVB + (tt * 2 + mt) * 512 + lane * 8) = cvt4h(va[mt]);
-    }
-    __syncthreads();  // the row's K / V pieces are in LDS
-
-    // ---- S^T[key][query] = K Q^T (log2 units) over the row's key tiles, softmax over keys, O^T = V^T P^T
+    for (int mt = 0; mt < 2; ++mt) *(f16x4*)(kx + KVB + (tt * 2 + mt) * 512 + lane * 8) = cvt4h(va[mt]);
+  };
+  // ---- attention of head h (exchange parity h & 1): S^T[key][query] = K Q^T (log2 units) over the row's key
+  //      tiles, softmax over keys, O^T = V^T P^T
+  auto attend = [&](int h, const f16x8& qf) __attribute__((always_inline)) {
+    const unsigned char* kx = kvx + (h & 1) * KVS + rl * 2 * KVB;
     f32x4 st[NT];
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt)
@@ -167,11 +165,26 @@ __global__ __launch_bounds__(64 * NT * FtRows<NT>::R, 1) void feat_tiles_kernel(
       }
     }
     of[h] = cat8h(oa[0], oa[1], inv);
-    __syncthreads();  // DMA of the next image landed; this head's weight buffer and exchange buffer are free
+  };
+  // software pipeline over heads, ONE barrier per head: step h runs the attention of head h (its K / V
+  // exchanged in step h-1) beside the projections of head h+1 (weights DMA'd during step h-1), and DMAs the
+  // image two heads ahead into the weight buffer head h's projections used (step h-1); the barrier ending step h
+  // publishes K / V(h+1), lands the next image and frees exchange parity h & 1 for head h+2.  The two work
+  // streams of a step are independent, so one wave's projection MFMAs fill the other's softmax latency.
+  f16x8 qcur, qnext;
+  dma(pack + FT_QKV_IMG, wbuf + FT_QKV_IMG, FT_PIECES);  // head 1 -> buffer 1
+  project(0, qcur);
+  __syncthreads();  // K / V(0) visible; head 1's image landed
+#pragma unroll
+  for (int h = 0; h < FT_H; ++h) {
+    // the image two heads ahead into buffer h & 1: head h+2's QKV, then the out-projection's halves
+    if (h + 2 < FT_H) dma(pack + (h + 2) * FT_QKV_IMG, wbuf + (h & 1) * FT_QKV_IMG, FT_PIECES);
+    else dma(pack + FT_H * FT_QKV_IMG + (h + 2 - FT_H) * FT_QKV_IMG, wbuf + (h & 1) * FT_QKV_IMG, FT_PIECES);
+    if (h + 1 < FT_H) project(h + 1, qnext);
+    attend(h, qcur);
+    qcur = qnext;
+    __syncthreads();
   }
-  // second half of the out-projection image (buffer 1, read by head 5 until the barrier above)
-  dma(pack + FT_H * FT_QKV_IMG + FT_QKV_IMG, wbuf + FT_QKV_IMG, FT_PIECES);
-  __syncthreads();
 
   // ---- Y^T = Wout . O^T over K = 192 (K-step h = head h), image [192][FT_ST] rows in f16_row_perm order,
   //      then residual (the tile's own X fragments) + LayerNorm per token (lane = token n, 48 of its features)
