@@ -60,9 +60,6 @@ struct mmpfn_cache {
 struct mmpfn_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  // PREC_F16 feature block: one wave per 16-token tile (feattile.hip, default) or one wave per row (featrow.hip,
-  // MMPFN_FEAT_KERNEL=rows at context creation; the two agree bitwise -- tests/test_parity_gpu.py)
-  bool feat_rows = false;
   // every stream bound since the last mmpfn_status: lanes run on their own streams and the NaN
   // flags they set must be read behind all of them
   std::vector<hipStream_t> seen_streams;
@@ -603,10 +600,7 @@ int feat_sublayer(mmpfn_ctx* ctx, const LayerW& L, void* Xv, int S, int T, int M
   unsigned char* big = (unsigned char*)ctx->ws_big.p;
   if (prec == PREC_F16) {  // fp16 state: the row-resident kernel only (embed keeps F16 to T <= 64)
     if (!L.feat_pack_f.p || T > 64) return fail(ctx, MMPFN_ERR_INVALID, "PREC_F16 needs E = 192, 6 heads, T <= 64");
-    if (!ctx->feat_rows)  // one wave per 16-token tile (feattile.hip)
-      HIPCHK(launch_feat_tiles(Xv, L.feat_pack_f.p, S, T, M, E, H, d.ln_eps, st));
-    else
-      HIPCHK(launch_feat_rows(Xv, L.feat_pack_f.p, S, T, M, E, H, d.ln_eps, st, true));
+    HIPCHK(launch_feat_rows(Xv, L.feat_pack_f.p, S, T, M, E, H, d.ln_eps, st, true));
     return MMPFN_OK;
   }
   float* Xall = (float*)Xv;
@@ -1025,8 +1019,6 @@ mmpfn_ctx* mmpfn_create(int device, void* stream) {
   if (hipSetDevice(device) != hipSuccess) return nullptr;
   mmpfn_ctx* c = new mmpfn_ctx();
   c->device = device;
-  const char* fk = std::getenv("MMPFN_FEAT_KERNEL");
-  c->feat_rows = fk && std::string(fk) == "rows";
   c->stream = (hipStream_t)stream;
   c->seen_streams.push_back(c->stream);
   return c;

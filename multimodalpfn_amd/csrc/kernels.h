@@ -151,9 +151,6 @@ hipError_t launch_proj3_resln(const float* O, const void* W, int64_t w_lo, int64
 // f16: PREC_F16 -- X fp16, pack the fp16 images with the out-projection rows permuted (pack_feat_rows res_perm)
 hipError_t launch_feat_rows(void* X, const void* pack, int S, int T, int M, int E, int H, float eps, hipStream_t st,
                             bool f16 = false);
-// the same sublayer on the fp16 state with one wave per 16-token tile (feattile.hip), the same weight pack as
-// launch_feat_rows(f16) and bitwise the same result
-hipError_t launch_feat_tiles(void* X, const void* pack, int S, int T, int M, int E, int H, float eps, hipStream_t st);
 
 // fused attention-between-features sublayer (bf16 only): X <- LN(X + MHA_feat(X)) per row,
 // wqkv [3*H*32][E] bf16, wout [E][H*32] bf16; rows per block = feat_block_rows(T) (0: unsupported T)

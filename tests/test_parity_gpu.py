@@ -831,33 +831,3 @@ def test_f16_mode_within_reference_fp16_deviation(case):
     check_argmax(out, r32, BF16_AGREE, f"f16 vs ref-f32 {case}")
     check_argmax(out, r16, BF16_AGREE, f"f16 vs ref-f16 {case}")
 
-
-@pytest.mark.parametrize("F,S,n_mod", [(9, 300, 0), (40, 517, 0), (80, 260, 0), (21, 2298, 1), (120, 130, 0)])
-def test_feature_tile_kernel_equals_row_kernel(F, S, n_mod, monkeypatch):
-    """PREC_F16's feature block as one wave per 16-token tile (feattile.hip, the default) against one wave per row
-    (featrow.hip, MMPFN_FEAT_KERNEL=rows): bitwise equal forwards at 1, 2, 3 and 4 tiles per row (T = 6, 21, 41,
-    36 with the image tokens, 61), two members batched, ragged row counts."""
-    from synth import synth_image, synth_labels, synth_state_dict, synth_table
-
-    from multimodalpfn_amd import _lib
-    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
-
-    cfg = ModelConfig(nlayers=2, mgm_heads=8, cap_heads=4)
-    sd = synth_state_dict(state_dict_spec(cfg), 31)
-    N = S * 4 // 5
-    x = synth_table(S, F, 31, n_cat=2)
-    y = synth_labels(S, 3, 31)[:N]
-    outs = []
-    for kernel in ("tiles", "rows"):
-        monkeypatch.setenv("MMPFN_FEAT_KERNEL", kernel)
-        eng = make_model(cfg, sd).engine()  # a fresh context reads the switch
-        tok = eng.mixer_tokens(torch.from_numpy(synth_image(S, n_mod, 31)).cuda(), _lib.PREC_F16) if n_mod else None
-        rng = np.random.default_rng(2)
-        items = [(torch.from_numpy(np.ascontiguousarray(x[:, rng.permutation(F)])), tok, y) for _ in range(2)]
-        with torch.inference_mode():
-            outs.append([o.cpu() for o in eng.forward_many(items, _lib.PREC_F16, lanes=1, batch=2)])
-            eng.status()
-        eng.close()
-    for a, b in zip(*outs):
-        assert torch.isfinite(a).all()
-        assert torch.equal(a, b)
