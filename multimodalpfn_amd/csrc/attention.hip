@@ -565,11 +565,6 @@ __device__ __attribute__((noinline)) void a3_exact_rows(const Attn2Args& p, cons
   }
 }
 
-// CHEAP (the default, MMPFN_X3_ATTN_CHEAP): the measured precision budget of DESIGN 5.7 -- S = K Q^T on ONE fp16
-// product (Q and K rounded to fp16; logits 2.3-4.8e-6 from the all-fp32 forward at configs B-E) and P.V on two
-// (P rounded to bf16 once, V split: Vl Ph + Vh Ph; 1.9-3.6e-6), the row sums over that same Ph: 8 + 16 MFMA-32 and
-// 8 MFMA-16 per tile-wave instead of 24 + 24 and 16.  !CHEAP: every operand split (three products each).
-template <bool CHEAP>
 __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2][A3_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -602,7 +597,6 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
   int qh[A3_NCH], qsrow[A3_NCH];
   bool qok[A3_NCH];
   bf16x8 qfh[A3_NCH][2], qfl[A3_NCH][2];
-  f16x8 qf16[A3_NCH][2];
 #pragma unroll
   for (int qb = 0; qb < A3_NCH; ++qb) {
     const int j = jw + 32 * qb + r;
@@ -616,15 +610,9 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
     }
     const float* qrow = (const float*)p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const f32x4 a = *(const f32x4*)(qrow + 16 * ks + 8 * hh), e = *(const f32x4*)(qrow + 16 * ks + 8 * hh + 4);
-      if constexpr (CHEAP) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) qf16[qb][ks][i] = (_Float16)(a[i] * c), qf16[qb][ks][4 + i] = (_Float16)(e[i] * c);
-      } else {
-        a3_split8(a, e, c, qfh[qb][ks], qfl[qb][ks]);
-      }
-    }
+    for (int ks = 0; ks < 2; ++ks)
+      a3_split8(*(const f32x4*)(qrow + 16 * ks + 8 * hh), *(const f32x4*)(qrow + 16 * ks + 8 * hh + 4), c,
+                qfh[qb][ks], qfl[qb][ks]);
   }
 
   const int ntiles = (p.nk + A2_KT - 1) / A2_KT;
@@ -651,16 +639,9 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
   auto lstore = [&](int buf) __attribute__((always_inline)) {
     unsigned char* Ks = lds[buf];
     bf16x8 hi, lo;
-    if constexpr (CHEAP) {  // K in fp16, one plane
-      f16x8 kk;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) kk[i] = (_Float16)rk[0][i], kk[4 + i] = (_Float16)rk[1][i];
-      *(f16x8*)(Ks + koff_w) = kk;
-    } else {
-      a3_split8(rk[0], rk[1], 1.0f, hi, lo);
-      *(bf16x8*)(Ks + koff_w) = hi;
-      *(bf16x8*)(Ks + 4096 + koff_w) = lo;
-    }
+    a3_split8(rk[0], rk[1], 1.0f, hi, lo);
+    *(bf16x8*)(Ks + koff_w) = hi;
+    *(bf16x8*)(Ks + 4096 + koff_w) = lo;
     a3_split8(rv[0], rv[1], 1.0f, hi, lo);
     const u32x4 vh = __builtin_bit_cast(u32x4, hi), vl = __builtin_bit_cast(u32x4, lo);
     *(u32x2*)(Ks + 8192 + voff_w0) = u32x2{vh.x, vh.y};
@@ -704,17 +685,12 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
     const unsigned char* Ks = lds[it & 1];
     if (active) {
       bf16x8 kh[2][2], kl[2][2], vh[2][2], vl[2][2];
-      f16x8 k16[2][2];
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          if constexpr (CHEAP) {
-            k16[u][i] = *(const f16x8*)(Ks + kro[u][i]);
-          } else {
-            kh[u][i] = *(const bf16x8*)(Ks + kro[u][i]);
-            kl[u][i] = *(const bf16x8*)(Ks + 4096 + kro[u][i]);
-          }
+          kh[u][i] = *(const bf16x8*)(Ks + kro[u][i]);
+          kl[u][i] = *(const bf16x8*)(Ks + 4096 + kro[u][i]);
           vh[u][i] = *(const bf16x8*)(Ks + vro[u][i]);
           vl[u][i] = *(const bf16x8*)(Ks + 4096 + vro[u][i]);
         }
@@ -723,11 +699,6 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
       for (int qb = 0; qb < A3_NCH; ++qb)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          if constexpr (CHEAP) {
-            s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k16[u][0], qf16[qb][0], zero16, 0, 0, 0);
-            s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k16[u][1], qf16[qb][1], s[qb][u], 0, 0, 0);
-            continue;
-          }
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[u][0], qfh[qb][0], zero16, 0, 0, 0);
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[u][1], qfh[qb][1], s[qb][u], 0, 0, 0);
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[u][0], qfl[qb][0], s[qb][u], 0, 0, 0);
@@ -774,13 +745,7 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
             for (int j = 0; j < 8; ++j) {
               const float e = __builtin_amdgcn_exp2f(s[qb][u][8 * sp + j]);
               ph[j] = (bf16)e;
-              if constexpr (!CHEAP) pl[j] = (bf16)(e - (float)ph[j]);
-            }
-            if constexpr (CHEAP) {
-              o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl[u][sp], ph, o[qb], 0, 0, 0);
-              o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[u][sp], ph, o[qb], 0, 0, 0);
-              lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, ph, lacc[qb], 0, 0, 0);
-              continue;
+              pl[j] = (bf16)(e - (float)ph[j]);
             }
             o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl[u][sp], ph, o[qb], 0, 0, 0);
             o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[u][sp], pl, o[qb], 0, 0, 0);
@@ -891,10 +856,7 @@ hipError_t launch_item_attention(const void* q, const void* k, const void* vt, v
   a.nblocks = acc * T;
   if (a.nblocks == 0) return hipSuccess;
   if (x3) {
-#ifndef MMPFN_X3_ATTN_CHEAP
-#define MMPFN_X3_ATTN_CHEAP 1
-#endif
-    hipLaunchKernelGGL((attn_item3_kernel<MMPFN_X3_ATTN_CHEAP != 0>), dim3(a.nblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(attn_item3_kernel, dim3(a.nblocks), dim3(256), 0, st, a);
     return hipGetLastError();
   }
   return launch_attn_pipe(a, st);

@@ -486,6 +486,12 @@ class ReshapeFeatureDistributionsStep(FeaturePreprocessingTransformerStep):
             parts.extend((f"transformer_{i}", rng.choice(choices), [i]) for i in targets)
 
         tf: Any = ColumnTransformer(parts, remainder="drop", sparse_threshold=0.0)
+        # a table that only passes columns through ("none" with no global transformer: run.py's members) is a
+        # column selection; predict takes it straight (identical values, ~1/50 of the ColumnTransformer's per-call
+        # cost, which sits in front of the first member's launch -- DESIGN 7)
+        ident = self.transform_name == "none" and not global_tf
+        self.select_cols_ = (self.subsampled_features_[np.concatenate([np.asarray(c, dtype=np.int64) for _, _, c in parts])]
+                             if ident and parts else None)
         if global_tf:
             tf = Pipeline([("preprocess", tf), ("global_transformer", global_tf)])
         self.transformer_ = tf
@@ -505,6 +511,9 @@ class ReshapeFeatureDistributionsStep(FeaturePreprocessingTransformerStep):
 
     def _transform(self, X: np.ndarray, *, is_test: bool = False) -> np.ndarray:
         assert self.transformer_ is not None, "You must call fit first"
+        sel = getattr(self, "select_cols_", None)
+        if sel is not None and isinstance(X, np.ndarray) and X.ndim == 2:
+            return X[:, sel]
         return self.transformer_.transform(X[:, self.subsampled_features_])
 
 

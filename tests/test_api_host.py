@@ -190,3 +190,31 @@ def test_numpy_predict_encoding_matches_pandas_route(name, tmp_path):
     slow = clf.preprocessor_.transform(_fix_dtypes(validate_X_predict(Xt, clf),
                                                    cat_indices=clf.categorical_features_indices))
     np.testing.assert_array_equal(fast, np.asarray(slow, dtype=np.float64))
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_passthrough_member_transform_fast_path(name, tmp_path):
+    """A member table that only passes columns through ("none" with no global transformer) is taken as a column
+    selection at predict (ReshapeFeatureDistributionsStep.select_cols_): the same values as its ColumnTransformer."""
+    from multimodalpfn_amd.model.preprocessing import ReshapeFeatureDistributionsStep
+
+    case = _case(name)
+    d = case_data(case)
+    if d["X_train"] is None:
+        pytest.skip("image-only case")
+    clf = make_classifier(case, write_ckpt(case, tmp_path), device="cpu")
+    clf.fit(d["X_train"], d["image_train"], d["y_train"])
+    Xe = clf._encode_predict_X(d["X_test"])
+    seen = 0
+    for pre in clf.executor_.preprocessors:
+        X = Xe
+        for step in pre:
+            if isinstance(step, ReshapeFeatureDistributionsStep):
+                fast = step._transform(X, is_test=True)
+                slow = step.transformer_.transform(X[:, step.subsampled_features_])
+                np.testing.assert_array_equal(fast, slow)
+                assert fast.dtype == slow.dtype
+                seen += step.select_cols_ is not None
+            X = step.transform(X).X
+    if name == "pad_none":
+        assert seen > 0  # run.py's members take the fast path
