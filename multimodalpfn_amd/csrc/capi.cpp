@@ -75,7 +75,7 @@ struct mmpfn_ctx {
   DevBuf enc_w, y_w, y_b, pe_w, pe_b, dec_w1, dec_b1, dec_w2, dec_b2;
   DevBuf dec_w1_h, dec_w1_f, dec_w2p_h, dec_w2p_f;  // 16-bit decoder: W1 [Fh][E], W2 [16][Fh] permuted
   // mixer
-  DevBuf mgm_w1, mgm_w1_h, mgm_b1, mgm_w2, mgm_w2_h, mgm_b2;
+  DevBuf mgm_w1, mgm_w1_h, mgm_w1_f, mgm_b1, mgm_w2, mgm_w2_h, mgm_w2_f, mgm_b2;
   DevBuf cap_qp, cap_kv, cap_kv_h, cap_kv_b, cap_o, cap_o_h, cap_o_b, cap_f0, cap_f0_h, cap_f0_b, cap_f3, cap_f3_h,
       cap_f3_b, cap_ng, cap_nb;
   DevBuf cap_f0_p, cap_f3_p, cap_vecs;  // E = 192: the FFN in mlp_rows order (bf16) and [bo | b0 | g | b + b3]
@@ -347,6 +347,10 @@ int finalize(mmpfn_ctx* ctx) {
     if ((rc = up2(ctx, ctx->mgm_w1, ctx->mgm_w1_h, W1))) return rc;
     if ((rc = upload(ctx, ctx->mgm_b1, B1, false))) return rc;
     if ((rc = up2(ctx, ctx->mgm_w2, ctx->mgm_w2_h, W2))) return rc;
+    if (E == 192 && (mg * D) % 256 == 0 && D % 64 == 0) {  // PREC_F16's head bank (the big-tile kernels only)
+      if ((rc = upload_f16(ctx, ctx->mgm_w1_f, W1))) return rc;
+      if ((rc = upload_f16(ctx, ctx->mgm_w2_f, W2))) return rc;
+    }
     if ((rc = upload(ctx, ctx->mgm_b2, B2, false))) return rc;
   }
   if (d.mixer_type == MMPFN_MIXER_MGM_CAP) {
@@ -850,24 +854,31 @@ int decode(mmpfn_ctx* ctx, float* logits, int M = 1) {
 }
 
 // MGM head bank (transformer.py:33-57): image [S][n_mod][D] -> tokens [S][mgm*n_mod][E] (head-major)
-// tok_bf16: the tokens in bf16 (the MGM+CAP chain's intermediate; bf16 mode, E = 192 only)
-int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, void* mtok, int prec, bool tok_bf16 = false) {
+// tok16: the tokens in 16-bit (the MGM+CAP chain's intermediate; bf16, or fp16 under PREC_F16; E = 192 only).
+// PREC_F16 runs the head bank on fp16 operands (LN output, GLU hidden, weights) where the big-tile kernels take
+// the shape, else in the bf16 mode: fp16's 3 extra mantissa bits cut the mixer's share of the logits error ~7x
+// (DESIGN 5.8), and the reference's own fp16 autocast runs these linears in fp16.
+bool mgm_f16(const mmpfn_ctx* ctx) { return ctx->mgm_w1_f.p != nullptr && ctx->d.nhid % 64 == 0; }
+
+int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, void* mtok, int prec, bool tok16 = false) {
   const mmpfn_model_desc& d = ctx->d;
   const int E = d.emsize, D = d.nhid;
-  const bool bf = prec == PREC_BF16;
+  if (prec == PREC_F16 && !mgm_f16(ctx)) prec = PREC_BF16;
+  const bool h = prec == PREC_F16, bf = prec == PREC_BF16 || h;
   const int eb = bf ? 2 : 4;
   hipStream_t st = ctx->stream;
   const int64_t rows = (int64_t)S * n_mod;
   const int mg = d.mgm_heads, M = mg * n_mod;
   RC(ensure(ctx, ctx->mx[0], (size_t)rows * D * eb));             // normalised image
   RC(ensure(ctx, ctx->mx[1], (size_t)rows * mg * (D / 2) * eb));  // GLU output
-  HIPCHK(launch_layernorm_rows(image, rows, D, 1e-5f, ctx->mx[0].p, !bf, nullptr, nullptr, st));
+  HIPCHK(launch_layernorm_rows(image, rows, D, 1e-5f, ctx->mx[0].p, !bf, nullptr, nullptr, st, h));
   GemmArgs a = gargs();
   a.A = ctx->mx[0].p, a.lda = D, setw(ctx, a, ctx->mgm_w1, ctx->mgm_w1_h, prec), a.bias = (const float*)ctx->mgm_b1.p;
   a.M = (int)rows, a.N = mg * D, a.K = D, a.C = ctx->mx[1].p, a.ldc = (int64_t)mg * (D / 2);
-  const bool big2 = bf && E == 192 && (D / 2) % 32 == 0;  // the big-tile down-projection (bf16 tokens possible)
+  const bool big2 = bf && E == 192 && (D / 2) % 32 == 0;  // the big-tile down-projection (16-bit tokens possible)
   if (bf && (mg * D) % 256 == 0 && D % 64 == 0)
-    HIPCHK(launch_gemm_glu_big(ctx->mx[0].p, a.W, a.bias, ctx->mx[1].p, (int)rows, mg * D, D, st));
+    HIPCHK(launch_gemm_glu_big(ctx->mx[0].p, h ? ctx->mgm_w1_f.p : a.W, a.bias, ctx->mx[1].p, (int)rows, mg * D, D,
+                               st, h));
   else
     HIPCHK(launch_gemm(a, prec, EPI_GLU, !bf, !bf, 1, st));
   GemmArgs b = gargs();
@@ -876,20 +887,23 @@ int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, void* mtok, 
   b.bias = (const float*)ctx->mgm_b2.p, b.b_zstride = E;
   b.M = (int)rows, b.N = E, b.K = D / 2;
   b.C = mtok, b.ldc = E, b.rdiv2 = n_mod, b.rmul2 = M, b.zmul = n_mod;
-  if (tok_bf16 && !big2) return fail(ctx, MMPFN_ERR_INVALID, "bf16 MGM tokens");
+  if (tok16 && !big2) return fail(ctx, MMPFN_ERR_INVALID, "16-bit MGM tokens");
   if (big2)
-    HIPCHK(launch_gemm_remap_big(ctx->mx[1].p, (int64_t)mg * (D / 2), ctx->mgm_w2_h.p, (const float*)ctx->mgm_b2.p, mtok,
-                                 tok_bf16, (int)rows, D / 2, mg, n_mod, E, st));
+    HIPCHK(launch_gemm_remap_big(ctx->mx[1].p, (int64_t)mg * (D / 2), h ? ctx->mgm_w2_f.p : ctx->mgm_w2_h.p,
+                                 (const float*)ctx->mgm_b2.p, mtok, tok16, (int)rows, D / 2, mg, n_mod, E, st, h));
   else
     HIPCHK(launch_gemm(b, prec, EPI_REMAP, !bf, true, mg, st));
   return MMPFN_OK;
 }
 
 // CrossAttentionPooler (transformer.py:60-88): MGM tokens [S][M][E] -> tokens [S][cap][E]
-// mtok fp32, or bf16 (in_bf16: from mixer_mgm's bf16 form)
-int mixer_cap(mmpfn_ctx* ctx, const void* mtok, int S, int M, float* tokens, int prec, bool in_bf16 = false) {
+// mtok fp32, or 16-bit (in16: from mixer_mgm's bf16 form, fp16 under PREC_F16); PREC_F16 runs the pooler in the
+// bf16 mode from the row pass on (its K|V, attention and tail stay bf16)
+int mixer_cap(mmpfn_ctx* ctx, const void* mtok, int S, int M, float* tokens, int prec, bool in16 = false) {
   const mmpfn_model_desc& d = ctx->d;
   const int E = d.emsize;
+  const bool in_f16 = in16 && prec == PREC_F16, in_bf16 = in16 && !in_f16;
+  if (prec == PREC_F16) prec = PREC_BF16;
   const bool bf = prec == PREC_BF16;
   const int eb = bf ? 2 : 4;
   hipStream_t st = ctx->stream;
@@ -905,7 +919,7 @@ int mixer_cap(mmpfn_ctx* ctx, const void* mtok, int S, int M, float* tokens, int
   void* vt = (char*)ctx->mx[4].p + (size_t)srows * E * 2;
   if (bf && E == 192) {  // k_norm + K|V projection in one row pass (normalised rows stay in registers)
     HIPCHK(launch_rowgemm_ln_store(mtok, in_bf16, ctx->cap_kv_h.p, (const float*)ctx->cap_kv_b.p, ctx->mx[4].p, srows,
-                                   2 * E, 1e-5f, true, st, mf ? vt : nullptr, E, M));
+                                   2 * E, 1e-5f, true, st, mf ? vt : nullptr, E, M, in_f16));
   } else {
     HIPCHK(launch_layernorm_rows((const float*)mtok, srows, E, 1e-5f, ctx->mx[3].p, !bf, nullptr, nullptr, st));
     GemmArgs c = gargs();
@@ -948,17 +962,20 @@ int mixer_cap(mmpfn_ctx* ctx, const void* mtok, int S, int M, float* tokens, int
 int mixer(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* tokens, int prec) {
   const mmpfn_model_desc& d = ctx->d;
   const int E = d.emsize, D = d.nhid;
-  const bool bf = prec == PREC_BF16;
-  const int eb = bf ? 2 : 4;
-  hipStream_t st = ctx->stream;
   if (d.mixer_type == MMPFN_MIXER_MGM) return mixer_mgm(ctx, image, S, n_mod, tokens, prec);
   if (d.mixer_type == MMPFN_MIXER_MGM_CAP) {
     const int M = d.mgm_heads * n_mod;
     RC(ensure(ctx, ctx->mx[2], (size_t)S * M * E * 4));
-    const bool tb = bf && E == 192 && (D / 2) % 32 == 0;  // bf16 intermediate tokens (half the HBM bytes)
+    if (prec == PREC_F16 && !mgm_f16(ctx)) prec = PREC_BF16;
+    const bool b16 = prec == PREC_BF16 || prec == PREC_F16;
+    const bool tb = b16 && E == 192 && (D / 2) % 32 == 0;  // 16-bit intermediate tokens (half the HBM bytes)
     RC(mixer_mgm(ctx, image, S, n_mod, ctx->mx[2].p, prec, tb));
     return mixer_cap(ctx, ctx->mx[2].p, S, M, tokens, prec, tb);
   }
+  if (prec == PREC_F16) prec = PREC_BF16;  // the MoE mixer runs the bf16 mode
+  const bool bf = prec == PREC_BF16;
+  const int eb = bf ? 2 : 4;
+  hipStream_t st = ctx->stream;
   if (d.mixer_type == MMPFN_MIXER_MOE) {
     const int ne = d.mgm_heads;
     RC(ensure(ctx, ctx->mx[0], (size_t)S * D * eb));
@@ -1045,7 +1062,8 @@ void mmpfn_destroy(mmpfn_ctx* ctx) {
   for (DevBuf* b : {&ctx->dec_w1_h, &ctx->dec_w1_f, &ctx->dec_w2p_h, &ctx->dec_w2p_f}) fr(*b);
   for (DevBuf* b : {&ctx->enc_w, &ctx->y_w, &ctx->y_b, &ctx->pe_w, &ctx->pe_b, &ctx->dec_w1, &ctx->dec_b1,
                     &ctx->dec_w2, &ctx->dec_b2, &ctx->mgm_w1, &ctx->mgm_w1_h, &ctx->mgm_b1, &ctx->mgm_w2,
-                    &ctx->mgm_w2_h, &ctx->mgm_b2, &ctx->cap_qp, &ctx->cap_kv, &ctx->cap_kv_h, &ctx->cap_kv_b,
+                    &ctx->mgm_w2_h, &ctx->mgm_b2, &ctx->mgm_w1_f, &ctx->mgm_w2_f, &ctx->cap_qp, &ctx->cap_kv,
+                    &ctx->cap_kv_h, &ctx->cap_kv_b,
                     &ctx->cap_o, &ctx->cap_o_h, &ctx->cap_o_b, &ctx->cap_f0, &ctx->cap_f0_h, &ctx->cap_f0_b,
                     &ctx->cap_f3, &ctx->cap_f3_h, &ctx->cap_f3_b, &ctx->cap_ng, &ctx->cap_nb, &ctx->cap_f0_p,
                     &ctx->cap_f3_p, &ctx->cap_vecs, &ctx->moe_w1, &ctx->moe_w1_h, &ctx->moe_b1, &ctx->moe_w2, &ctx->moe_w2_h, &ctx->moe_b2, &ctx->moe_gw,
@@ -1132,9 +1150,9 @@ int mmpfn_mixer_forward(mmpfn_ctx* ctx, const float* image, int S, int n_mod, fl
   if (!ctx->finalized) return fail(ctx, MMPFN_ERR_STATE, "weights not finalised");
   if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
-  // (PREC_F16 projects the modality tokens in the bf16 mode: they enter the state through the fp32 encoders)
-  const int bp = base_prec(precision);
-  return mixer(ctx, image, S, n_mod, tokens, bp == PREC_F16 ? PREC_BF16 : bp);
+  // (PREC_F16: the MGM head bank on fp16 operands, the pooler and MoE in the bf16 mode; the tokens enter the state
+  // through the fp32 encoders)
+  return mixer(ctx, image, S, n_mod, tokens, base_prec(precision));
 }
 
 int mmpfn_embed(mmpfn_ctx* ctx, const float* x, int S, int F, const float* tokens, int C, const float* y, int N,
@@ -1427,7 +1445,7 @@ int mmpfn_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, float* token
   if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
   const int bp = base_prec(precision);
-  return mixer_mgm(ctx, image, S, n_mod, tokens, bp == PREC_F16 ? PREC_BF16 : bp);
+  return mixer_mgm(ctx, image, S, n_mod, tokens, bp);
 }
 
 int mmpfn_cap(mmpfn_ctx* ctx, const float* mgm_tokens, int S, int M, float* tokens, int precision) {
@@ -1437,7 +1455,7 @@ int mmpfn_cap(mmpfn_ctx* ctx, const float* mgm_tokens, int S, int M, float* toke
   if (!prec_ok(precision)) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
   const int bp = base_prec(precision);
-  return mixer_cap(ctx, mgm_tokens, S, M, tokens, bp == PREC_F16 ? PREC_BF16 : bp);
+  return mixer_cap(ctx, mgm_tokens, S, M, tokens, bp);
 }
 
 }  // extern "C"

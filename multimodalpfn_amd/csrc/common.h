@@ -78,6 +78,7 @@ __device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f32(float x);
 template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+template <> __device__ __forceinline__ _Float16 from_f32<_Float16>(float x) { return (_Float16)x; }
 
 // erf, branch-free (Abramowitz & Stegun 7.1.26, |abs err| <= 1.5e-7): the libm
 // erff is a multi-branch routine that dominated the MLP epilogue.

@@ -434,9 +434,15 @@ __device__ __forceinline__ void gb_dma16(const void* src, unsigned lds_base) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_base) : "memory");
 }
 
-__global__ __launch_bounds__(512, 1) void gemm_glu_big_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
-                                                              const float* __restrict__ bias, bf16* __restrict__ C,
-                                                              int M, int N, int K, int mtiles) {
+// F16: the same kernel on fp16 operands (the fp16 mode's mixer: the reference's autocast runs these Linears in fp16)
+template <bool F16>
+__global__ __launch_bounds__(512, 1) void gemm_glu_big_kernel(const typename Op16<F16>::t* __restrict__ A,
+                                                              const typename Op16<F16>::t* __restrict__ W,
+                                                              const float* __restrict__ bias,
+                                                              typename Op16<F16>::t* __restrict__ C, int M, int N, int K,
+                                                              int mtiles) {
+  typedef typename Op16<F16>::t T;
+  typedef typename Op16<F16>::x8 X8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -456,7 +462,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glu_big_kernel(const bf16* __rest
 
   // DMA piece j of this wave: LDS chunk q = (wave * GB_DMA + j) * 64 + lane of the stage image
   // (rows 0-255 = A, 256-511 = W); row r = q / 4 holds global chunk c with gb_slot(r, c) = q % 4
-  const bf16* src[GB_DMA];
+  const T* src[GB_DMA];
 #pragma unroll
   for (int j = 0; j < GB_DMA; ++j) {
     const int q = (wave * GB_DMA + j) * 64 + lane, r = q >> 2, c = gb_slot(r, q & 3);
@@ -490,25 +496,25 @@ __global__ __launch_bounds__(512, 1) void gemm_glu_big_kernel(const bf16* __rest
     if (kt + GB_NST - 1 < nk) dma(kt + GB_NST - 1);
     const unsigned char* As = smem + (kt % GB_NST) * GB_STAGE;
     const unsigned char* Ws = As + GB_M * GB_ROW;
-    bf16x8 af[GB_MT], bw[4];
+    X8 af[GB_MT], bw[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rb = wn * 64 + i * 16 + fr;
-      bw[i] = *(const bf16x8*)(Ws + rb * GB_ROW + 16 * gb_slot(rb, fg));
+      bw[i] = *(const X8*)(Ws + rb * GB_ROW + 16 * gb_slot(rb, fg));
     }
 #pragma unroll
     for (int i = 0; i < GB_MT; ++i) {
       const int ra = wm * (GB_M / 2) + i * 16 + fr;
-      af[i] = *(const bf16x8*)(As + ra * GB_ROW + 16 * gb_slot(ra, fg));
+      af[i] = *(const X8*)(As + ra * GB_ROW + 16 * gb_slot(ra, fg));
     }
 #pragma unroll
     for (int a = 0; a < GB_MT; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bw[b], acc[a][b], 0, 0, 0);
+      for (int b = 0; b < 4; ++b) acc[a][b] = mfma16x(af[a], bw[b], acc[a][b]);
   }
   __syncthreads();  // every wave is done with the ring before it is reused for the output tile
   // GLU epilogue: C tile lane layout (row 16a + 4fg + r, column fr of tile b); a = tile 2q, b = 2q+1
-  bf16* Ct = (bf16*)smem;  // [GB_M][GB_OST]
+  T* Ct = (T*)smem;  // [GB_M][GB_OST]
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int na = n0 + wn * 64 + q * 32 + fr;
@@ -518,7 +524,7 @@ __global__ __launch_bounds__(512, 1) void gemm_glu_big_kernel(const bf16* __rest
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float va = acc[a][2 * q][r] + ba, vb = acc[a][2 * q + 1][r] + bb;
-        Ct[(wm * (GB_M / 2) + a * 16 + fg * 4 + r) * GB_OST + wn * 32 + q * 16 + fr] = (bf16)(va * sigmoidf_(vb));
+        Ct[(wm * (GB_M / 2) + a * 16 + fg * 4 + r) * GB_OST + wn * 32 + q * 16 + fr] = (T)(va * sigmoidf_(vb));
       }
   }
   __syncthreads();
@@ -544,11 +550,14 @@ static_assert(GR_M + GR_N == GB_M + GB_N, "four DMA pieces per thread and K slic
 constexpr int GR_MT = GR_M / 32;  // 16-row tiles per wave (10)
 constexpr int GR_NT = GR_N / 64;  // 16-column tiles per wave (3)
 
-template <typename TO>  // fp32 tokens, or bf16 (the MGM+CAP chain's intermediate, read by the CAP K|V projection)
-__global__ __launch_bounds__(512, 1) void gemm_remap_big_kernel(const bf16* __restrict__ A, int64_t lda,
-                                                                const bf16* __restrict__ W,
+// TO: fp32 tokens, or 16-bit (the MGM+CAP chain's intermediate, read by the CAP K|V projection); F16: fp16 operands
+template <typename TO, bool F16>
+__global__ __launch_bounds__(512, 1) void gemm_remap_big_kernel(const typename Op16<F16>::t* __restrict__ A, int64_t lda,
+                                                                const typename Op16<F16>::t* __restrict__ W,
                                                                 const float* __restrict__ bias, TO* __restrict__ C,
                                                                 int M, int K, int mtiles, int n_mod, int Mtok) {
+  typedef typename Op16<F16>::t T;
+  typedef typename Op16<F16>::x8 X8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -563,7 +572,7 @@ __global__ __launch_bounds__(512, 1) void gemm_remap_big_kernel(const bf16* __re
   }
   const int m0 = mt * GR_M;
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
-  const bf16* src[GB_DMA];
+  const T* src[GB_DMA];
 #pragma unroll
   for (int j = 0; j < GB_DMA; ++j) {
     const int q = (wave * GB_DMA + j) * 64 + lane, r = q >> 2, c = gb_slot(r, q & 3);
@@ -595,21 +604,21 @@ __global__ __launch_bounds__(512, 1) void gemm_remap_big_kernel(const bf16* __re
     if (kt + GB_NST - 1 < nk) dma(kt + GB_NST - 1);
     const unsigned char* As = smem + (kt % GB_NST) * GB_STAGE;
     const unsigned char* Ws = As + GR_M * GB_ROW;
-    bf16x8 af[GR_MT], bw[GR_NT];
+    X8 af[GR_MT], bw[GR_NT];
 #pragma unroll
     for (int i = 0; i < GR_NT; ++i) {
       const int rb = wn * (GR_N / 4) + i * 16 + fr;
-      bw[i] = *(const bf16x8*)(Ws + rb * GB_ROW + 16 * gb_slot(rb, fg));
+      bw[i] = *(const X8*)(Ws + rb * GB_ROW + 16 * gb_slot(rb, fg));
     }
 #pragma unroll
     for (int i = 0; i < GR_MT; ++i) {
       const int ra = wm * (GR_M / 2) + i * 16 + fr;
-      af[i] = *(const bf16x8*)(As + ra * GB_ROW + 16 * gb_slot(ra, fg));
+      af[i] = *(const X8*)(As + ra * GB_ROW + 16 * gb_slot(ra, fg));
     }
 #pragma unroll
     for (int a = 0; a < GR_MT; ++a)
 #pragma unroll
-      for (int b = 0; b < GR_NT; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bw[b], acc[a][b], 0, 0, 0);
+      for (int b = 0; b < GR_NT; ++b) acc[a][b] = mfma16x(af[a], bw[b], acc[a][b]);
   }
   // C tile lane layout: row 16a + 4fg + r, column 16b + fr of the wave's 160 x 48 block; + b2[z], row remap
 #pragma unroll
@@ -652,31 +661,43 @@ hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool ou
 }
 
 hipError_t launch_gemm_remap_big(const void* A, int64_t lda, const void* W, const float* bias, void* C, bool c_bf16,
-                                 int M, int K, int nheads, int n_mod, int E, hipStream_t st) {
+                                 int M, int K, int nheads, int n_mod, int E, hipStream_t st, bool f16) {
   if (M <= 0) return hipSuccess;
   if (E != GR_N || K % GB_K != 0 || K <= 0 || nheads <= 0 || n_mod <= 0) return hipErrorInvalidValue;
   const int mtiles = (M + GR_M - 1) / GR_M;
   const int64_t nb = (int64_t)mtiles * nheads;
   const int lds = GB_NST * GB_STAGE;
-  if (c_bf16)
-    hipLaunchKernelGGL((gemm_remap_big_kernel<bf16>), dim3((unsigned)nb), dim3(512), lds, st, (const bf16*)A, lda,
+  if (f16) {  // fp16 operands; a 16-bit token output is fp16 too
+    if (c_bf16)
+      hipLaunchKernelGGL((gemm_remap_big_kernel<_Float16, true>), dim3((unsigned)nb), dim3(512), lds, st,
+                         (const _Float16*)A, lda, (const _Float16*)W, bias, (_Float16*)C, M, K, mtiles, n_mod, nheads * n_mod);
+    else
+      hipLaunchKernelGGL((gemm_remap_big_kernel<float, true>), dim3((unsigned)nb), dim3(512), lds, st,
+                         (const _Float16*)A, lda, (const _Float16*)W, bias, (float*)C, M, K, mtiles, n_mod, nheads * n_mod);
+  } else if (c_bf16) {
+    hipLaunchKernelGGL((gemm_remap_big_kernel<bf16, false>), dim3((unsigned)nb), dim3(512), lds, st, (const bf16*)A, lda,
                        (const bf16*)W, bias, (bf16*)C, M, K, mtiles, n_mod, nheads * n_mod);
-  else
-    hipLaunchKernelGGL((gemm_remap_big_kernel<float>), dim3((unsigned)nb), dim3(512), lds, st, (const bf16*)A, lda,
-                       (const bf16*)W, bias, (float*)C, M, K, mtiles, n_mod, nheads * n_mod);
+  } else {
+    hipLaunchKernelGGL((gemm_remap_big_kernel<float, false>), dim3((unsigned)nb), dim3(512), lds, st, (const bf16*)A,
+                       lda, (const bf16*)W, bias, (float*)C, M, K, mtiles, n_mod, nheads * n_mod);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_gemm_glu_big(const void* A, const void* W, const float* bias, void* C, int M, int N, int K,
-                               hipStream_t st) {
+                               hipStream_t st, bool f16) {
   if (M <= 0) return hipSuccess;
   if (N % GB_N != 0 || K % GB_K != 0 || K <= 0) return hipErrorInvalidValue;
   const int mtiles = (M + GB_M - 1) / GB_M;
   const int64_t nb = (int64_t)mtiles * (N / GB_N);
   const int lds = GB_NST * GB_STAGE;  // 144 KB
   static_assert(GB_M * GB_OST * 2 <= GB_NST * GB_STAGE, "output staging fits the ring");
-  hipLaunchKernelGGL(gemm_glu_big_kernel, dim3((unsigned)nb), dim3(512), lds, st, (const bf16*)A, (const bf16*)W,
-                     bias, (bf16*)C, M, N, K, mtiles);
+  if (f16)
+    hipLaunchKernelGGL((gemm_glu_big_kernel<true>), dim3((unsigned)nb), dim3(512), lds, st, (const _Float16*)A,
+                       (const _Float16*)W, bias, (_Float16*)C, M, N, K, mtiles);
+  else
+    hipLaunchKernelGGL((gemm_glu_big_kernel<false>), dim3((unsigned)nb), dim3(512), lds, st, (const bf16*)A,
+                       (const bf16*)W, bias, (bf16*)C, M, N, K, mtiles);
   return hipGetLastError();
 }
 

@@ -80,14 +80,15 @@ struct GemmArgs {
 hipError_t launch_gemm(const GemmArgs& a, int prec, int epi, bool a_f32, bool out_f32, int groups,
                        hipStream_t st);
 
-// MGM head bank, bf16: C[M][N/2] = GLU(A[M][K] . W^T + bias) with W rows GLU-interleaved in 16-row
+// MGM head bank, bf16 (fp16 with f16: A, W and C fp16): C[M][N/2] = GLU(A[M][K] . W^T + bias) with W rows GLU-interleaved in 16-row
 // blocks (capi.cpp); large-tile, XCD-ordered (gemm.hip gemm_glu_big_kernel); N % 256 == 0, K % 64 == 0
 // MGM per-head down-projection (bf16, E = 192): C[(r / n_mod) * nheads n_mod + z n_mod + r % n_mod][E] =
-// A[r][z K .. z K + K) (row stride lda) . W[z][E][K]^T + bias[z][E]; C fp32 or bf16 (c_bf16)
+// A[r][z K .. z K + K) (row stride lda) . W[z][E][K]^T + bias[z][E]; C fp32 or bf16 (c_bf16); with f16, A and W
+// fp16 and C fp32 or fp16 (c_bf16)
 hipError_t launch_gemm_remap_big(const void* A, int64_t lda, const void* W, const float* bias, void* C, bool c_bf16,
-                                 int M, int K, int nheads, int n_mod, int E, hipStream_t st);
+                                 int M, int K, int nheads, int n_mod, int E, hipStream_t st, bool f16 = false);
 hipError_t launch_gemm_glu_big(const void* A, const void* W, const float* bias, void* C, int M, int N, int K,
-                               hipStream_t st);
+                               hipStream_t st, bool f16 = false);
 
 // fused MLP sublayer: X <- LN(X + GELU(X W1^T) W2^T), W1 [Fh][E], W2 [E][Fh] in compute dtype
 hipError_t launch_mlp_fused(float* X, const void* W1, const void* W2, int64_t M, int E, int Fh, float eps, int prec,
@@ -117,12 +118,12 @@ hipError_t launch_rowgemm_qkv_pair(const void* X, int64_t rdiv1, int64_t roff1, 
                                    int64_t rdiv2, int64_t roff2, const void* W2, int M2, int N2, int64_t a_rmul,
                                    void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st,
                                    bool f16 = false);
-// C = (ln ? LayerNorm(A) : A) . W^T + bias: A fp32 or bf16 [M][192], W [N][192] bf16, C bf16 [M][N], N % 64 == 0;
+// C = (ln ? LayerNorm(A) : A) . W^T + bias: A fp32, bf16 or fp16 (a_f16) [M][192], W [N][192] bf16, C bf16 [M][N], N % 64 == 0;
 // with CT: outputs [vt_from, N) transposed per group of Mk rows into CT [M / Mk][N - vt_from][Mk] (Mk % 32 == 0),
 // C then [M][vt_from]
 hipError_t launch_rowgemm_ln_store(const void* A, bool a_bf16, const void* W, const float* bias, void* C, int64_t M,
                                    int N, float eps, bool ln, hipStream_t st, void* CT = nullptr, int vt_from = -1,
-                                   int Mk = 0);
+                                   int Mk = 0, bool a_f16 = false);
 hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, void* X, float eps, hipStream_t st,
                                 bool f16 = false);
 
@@ -260,7 +261,7 @@ hipError_t launch_aggregate(const float* logits /*[M][Q][n_out]*/, int M, int Q,
 
 // ---- mixer helpers -----------------------------------------------------------------
 hipError_t launch_layernorm_rows(const float* in, int64_t rows, int dim, float eps, void* out, bool out_f32,
-                                 const float* gamma, const float* beta, hipStream_t st);
+                                 const float* gamma, const float* beta, hipStream_t st, bool out_f16 = false);
 hipError_t launch_cap_attention(const float* qp /*[cap][E]*/, const void* kv /*[S][M][2E]*/, bool kv_f32,
                                 void* out /*[S][cap][E] fp32, or bf16 (out_bf16)*/, bool out_bf16, int S, int M, int cap,
                                 int E, hipStream_t st);

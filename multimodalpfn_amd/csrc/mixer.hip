@@ -337,7 +337,7 @@ __global__ void scale_tokens_kernel(float* __restrict__ tok, const float* __rest
 }  // namespace
 
 hipError_t launch_layernorm_rows(const float* in, int64_t rows, int dim, float eps, void* out, bool out_f32,
-                                 const float* gamma, const float* beta, hipStream_t st) {
+                                 const float* gamma, const float* beta, hipStream_t st, bool out_f16) {
   if (rows <= 0) return hipSuccess;
   dim3 grid((rows + 3) / 4);
   const int v4 = dim % 4 ? 0 : (dim / 4 + 63) / 64;  // float4 registers per lane
@@ -354,6 +354,7 @@ hipError_t launch_layernorm_rows(const float* in, int64_t rows, int dim, float e
     else go(tag, std::integral_constant<int, 0>{});
   };
   if (out_f32) pick(float{});
+  else if (out_f16) pick(_Float16{});
   else pick(bf16{});
   return hipGetLastError();
 }

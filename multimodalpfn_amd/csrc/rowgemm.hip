@@ -367,7 +367,11 @@ __global__ __launch_bounds__(256, 2) void rowgemm_ln_store_kernel(const TA* __re
     f32x4 lo[GE / 32], hi[GE / 32];
 #pragma unroll
     for (int ks = 0; ks < GE / 32; ++ks) {
-      if constexpr (sizeof(TA) == 2) {
+      if constexpr (std::is_same_v<TA, _Float16>) {  // the fp16 mode's MGM tokens
+        const f16x8 v = *(const f16x8*)(xr + ks * 32);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lo[ks][i] = (float)v[i], hi[ks][i] = (float)v[4 + i];
+      } else if constexpr (sizeof(TA) == 2) {
         const bf16x8 v = *(const bf16x8*)(xr + ks * 32);
 #pragma unroll
         for (int i = 0; i < 4; ++i) lo[ks][i] = (float)v[i], hi[ks][i] = (float)v[4 + i];
@@ -604,14 +608,18 @@ hipError_t launch_rowgemm_resln(const void* O, const void* W, int64_t M, void* X
 }
 
 hipError_t launch_rowgemm_ln_store(const void* A, bool a_bf16, const void* W, const float* bias, void* C, int64_t M,
-                                   int N, float eps, bool ln, hipStream_t st, void* CT, int vt_from, int Mk) {
+                                   int N, float eps, bool ln, hipStream_t st, void* CT, int vt_from, int Mk,
+                                   bool a_f16) {
   if (M <= 0) return hipSuccess;
   if (N % QC != 0 || N <= 0 || M > INT32_MAX) return hipErrorInvalidValue;
   if (CT && (vt_from < 0 || vt_from % QC != 0 || vt_from >= N || Mk <= 0 || Mk % 32 != 0 || M % Mk != 0))
     return hipErrorInvalidValue;
   const int ldc = CT ? vt_from : N;
   const dim3 grid((unsigned)((M + GROWS - 1) / GROWS));
-  if (a_bf16)
+  if (a_f16)
+    hipLaunchKernelGGL((rowgemm_ln_store_kernel<_Float16>), grid, dim3(256), 0, st, (const _Float16*)A, (const bf16*)W,
+                       bias, (bf16*)C, (int)M, N, eps, ln ? 1 : 0, ldc, (bf16*)CT, CT ? vt_from : -1, CT ? Mk : 1);
+  else if (a_bf16)
     hipLaunchKernelGGL((rowgemm_ln_store_kernel<bf16>), grid, dim3(256), 0, st, (const bf16*)A, (const bf16*)W, bias,
                        (bf16*)C, (int)M, N, eps, ln ? 1 : 0, ldc, (bf16*)CT, CT ? vt_from : -1, CT ? Mk : 1);
   else
