@@ -65,7 +65,7 @@ def parse():
     p.add_argument("--batch", type=int, default=None, help="members per batched forward (default: engine's)")
     p.add_argument("--mixer-stream", action="store_true",
                    help="headline step: the mixer on its own stream, overlapping the previous step's forwards")
-    p.add_argument("--api-steps", type=int, default=3, help="timed predict_proba calls of the API leg (0: skip)")
+    p.add_argument("--api-steps", type=int, default=10, help="timed predict_proba calls of the API leg (0: skip)")
     p.add_argument("--no-kv-cache", dest="kv_cache", action="store_false", help="skip the fit_with_cache leg")
     p.add_argument("--no-config-d", dest="config_d", action="store_false", help="skip the config-D leg")
     p.add_argument("--no-config-b", dest="config_b", action="store_false",
@@ -113,9 +113,10 @@ def attn_traffic(T):
     """HBM bytes per attention launch over T token columns, from the committed PMC pass
     (tools/attn_pmc.sh: rocprofv3 FETCH_SIZE and WRITE_SIZE runs at that launch shape)."""
     H, d, S, N = 6, 32, S_ROWS, N_TRAIN
-    # the shipped kernel's own pass only: the fp16 mode's launch (round 4) first, then the bf16 one (round 3;
-    # older rounds measured attn_item2)
-    cands = sorted((ROOT / "profiles" / "r04").glob("attn_pipe_pmc_T*_f16.json")) + \
+    # the shipped kernel's own pass only, newest first: the fp16 mode's launch (rounds 5, 4), then the bf16 one
+    # (round 3; older rounds measured attn_item2)
+    cands = sorted((ROOT / "profiles" / "r05").glob("attn_pipe_pmc_T*_f16.json")) + \
+        sorted((ROOT / "profiles" / "r04").glob("attn_pipe_pmc_T*_f16.json")) + \
         sorted((ROOT / "profiles" / "r03").glob("attn_pipe_pmc_T*[0-9].json"))
     for pmc in cands:
         rec = json.loads(pmc.read_text())
@@ -332,7 +333,8 @@ def api_end_to_end(cfg, sd, x, y, image, n_estimators, prec_f32, steps, world, p
         clf.fit(X[:N_TRAIN], image[:N_TRAIN], labels[:N_TRAIN])
         t_fit = time.perf_counter() - t0
     Xq, imq = X[N_TRAIN:], image[N_TRAIN:]
-    clf.predict_proba(Xq, imq)  # warm-up (engine build, weight upload)
+    for _ in range(3):  # warm-up (engine build, weight upload, the allocator's pinned / device blocks)
+        clf.predict_proba(Xq, imq)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()

@@ -260,6 +260,9 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
     def predict_proba_device(self, X, image_test: np.ndarray | None) -> torch.Tensor:
         """Class probabilities ``[Q, n_classes]`` fp32 left on the GPU (no rounding)."""
         check_is_fitted(self)
+        if image_test is not None and hasattr(self.executor_, "launch_mixer_early"):
+            # the mixer first: it does not need X, so the host's validation / encoding of X runs under it
+            self.executor_.launch_mixer_early(image_test, device=self.device_, autocast=self.use_autocast_)
         if X is not None:
             X = self._encode_predict_X(X)
         logits, perms = [], []

@@ -72,6 +72,33 @@ def test_predict_proba_16bit_close(name, mode, tmp_path, monkeypatch):
     check_argmax(proba, z["proba"], 0.995, f"api {name} {mode}")
 
 
+@pytest.mark.parametrize("fit_mode", ["fit_preprocessors", "low_memory"])
+def test_early_mixer_launch(fit_mode, tmp_path, monkeypatch):
+    """predict_proba enqueues the test rows' modality tokens before it validates / encodes X
+    (``InferenceEngine.launch_mixer_early``); the member loop must take exactly those tokens, and the result must
+    equal the predict without the early launch bitwise.  An image of the wrong width is left to the regular path
+    and its error."""
+    from multimodalpfn_amd import inference
+
+    case = _case("pad_none")
+    d = case_data(case)
+    clf = make_classifier(case, write_ckpt(case, tmp_path), inference_precision=torch.float32, fit_mode=fit_mode)
+    clf.fit(d["X_train"], d["image_train"], d["y_train"])
+    calls = []
+    orig = inference._mixer_tokens
+    monkeypatch.setattr(inference, "_mixer_tokens", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    a = clf.predict_proba(d["X_test"], d["image_test"])
+    assert len(calls) == 1 and clf.executor_._early_tokens is None
+    monkeypatch.setattr(type(clf.executor_), "launch_mixer_early", lambda self, *a, **k: None)
+    b = clf.predict_proba(d["X_test"], d["image_test"])
+    assert len(calls) == 2
+    np.testing.assert_array_equal(a, b)
+    monkeypatch.undo()
+    bad = np.concatenate([d["image_test"], d["image_test"][..., :1]], axis=-1)
+    with pytest.raises(ValueError):
+        clf.predict_proba(d["X_test"], bad)
+
+
 def test_low_memory_mode_is_reproducible(tmp_path):
     """``low_memory`` re-fits members at every predict from one fixed seed (inference.py:148)."""
     case = _case("pad_none")

@@ -21,8 +21,11 @@ g = torch.Generator().manual_seed(0)
 # ATT_PREC=f16: the fp16 mode's kernel (q, k, out fp16, V^T bf16; the headline's launch), else bf16
 f16 = os.environ.get("ATT_PREC", "bf16") == "f16"
 qdt = torch.float16 if f16 else torch.bfloat16
-q = torch.randn(T, H, S, d, generator=g).cuda().to(qdt)
-k = torch.randn(T, H, Npad, d, generator=g).cuda().to(qdt)
+q = torch.randn(T, H, S, d, generator=g).cuda()
+k = torch.randn(T, H, Npad, d, generator=g).cuda()
+if os.environ.get("ATT_QROUND") == "bf16":  # fp16 operands holding bf16 values: the same bits toggle as in bf16 mode
+    q, k = q.bfloat16().float(), k.bfloat16().float()
+q, k = q.to(qdt), k.to(qdt)
 vt = torch.randn(T, H, d, Npad, generator=g).cuda().bfloat16()
 o = torch.empty(T, S, H * d, device="cuda", dtype=qdt)
 st = torch.cuda.current_stream()
