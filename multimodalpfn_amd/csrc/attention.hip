@@ -831,7 +831,7 @@ namespace {
 hipError_t launch_item_attention(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
                                  int Npad, int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st,
                                  int64_t kv_bstride, bool q_prescaled, bool x3, const void* vt8 = nullptr,
-                                 int f8 = 0, bool qk_f16 = false) {
+                                 int f8 = 0, bool qk_f16 = false, bool o_f16 = false) {
   if (na + nb <= 0 || T <= 0) return hipSuccess;
   if (nk <= 0 || Npad % A2_KT != 0 || nk > Npad || H > 8 || H <= 0) return hipErrorInvalidValue;
   if (nb > 0 && (kvb < 0 || kvb >= H)) return hipErrorInvalidValue;
@@ -843,6 +843,7 @@ hipError_t launch_item_attention(const void* q, const void* k, const void* vt, v
   a.q_prescaled = q_prescaled ? 1 : 0;
   a.vt8 = (const unsigned char*)vt8, a.f8 = x3 ? 0 : f8;
   a.qk_f16 = (!x3 && qk_f16) ? 1 : 0;
+  a.o_f16 = (!x3 && (qk_f16 || o_f16)) ? 1 : 0;
   if (kv_bstride > 0 && (na > 0 || kvb != 0)) return hipErrorInvalidValue;  // cache layout holds head 0 only
   const int qpb = x3 ? A3_QPB : ATTN_ITEM_QPB;
   int acc = 0;
@@ -866,9 +867,9 @@ hipError_t launch_item_attention(const void* q, const void* k, const void* vt, v
 
 hipError_t launch_attn_layer(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride,
-                             bool q_prescaled, const void* vt8, int f8, bool qk_f16) {
+                             bool q_prescaled, const void* vt8, int f8, bool qk_f16, bool o_f16) {
   return launch_item_attention(q, k, vt, out, S, T, H, Npad, nk, a0, na, b0, nb, kvb, st, kv_bstride, q_prescaled,
-                               false, vt8, f8, qk_f16);
+                               false, vt8, f8, qk_f16, o_f16);
 }
 
 hipError_t launch_attn_item3(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,

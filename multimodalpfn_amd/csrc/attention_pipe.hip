@@ -30,8 +30,11 @@
 // tile's max (the first tile's max lands at 2^ETOP); a later score beyond the format's range converts to
 // NaN / inf, which the row-sum check catches, and the wave re-runs on the exact bf16 path.
 //
-// QF16 (PREC_F16): Q / K and the output O in fp16, so S = K Q^T runs on v_mfma_f32_32x32x16_f16 (same
-// rate); V^T and P stay bf16 (P = exp2(s) under the fixed reference needs bf16's exponent range).
+// QF16: Q / K in fp16, so S = K Q^T runs on v_mfma_f32_32x32x16_f16; OF16: the output O in fp16 (the fp16 mode's
+// state); V^T and P stay bf16 (P = exp2(s) under the fixed reference needs bf16's exponent range).  The fp16
+// mode's forward runs <F8, false, true> -- Q / K in bf16, so every MFMA of the loop is a bf16 one: with fp16 S
+// MFMAs between the bf16 P.V / row-sum MFMAs the same launch took 1.7 % longer on identical operand bits
+// (DESIGN 5.7); the kernel-level tap with fp16 Q / K (mmpfn_item_attention_layer_ex codes 5-7) runs <F8, true, true>.
 #include <type_traits>
 
 #include "common.h"
@@ -40,6 +43,33 @@
 namespace mmpfn {
 
 namespace {
+
+#ifdef MMPFN_STAMPS  // per-phase cycle stamps (diagnostics build only: make dbg; tools/attn_stamps.py)
+// 8 consecutive blocks from the grid's middle (consecutive block ids sit on the 8 XCDs), their 4 waves, AP_NST stamps
+// each (s_memtime, shader cycles): 0 kernel start, 1 Q fragments loaded, 2 prologue barrier passed (tiles 0-1 in
+// LDS), 3 + t after step t's barrier (t < AP_NST - 6), AP_NST - 3 after the loop's drain, AP_NST - 2 after the
+// row-sum check (and any re-run), AP_NST - 1 after the output stores
+constexpr int AP_NST = 48;
+__device__ unsigned long long g_ap_stamps[8 * 4 * AP_NST];
+__device__ int g_ap_meta[4];  // gridDim.x, ntiles of the first stamped block, the first stamped block id
+#define AP_STAMP(k)                                                                                     \
+  do {                                                                                                  \
+    const int sb_ = (int)blockIdx.x - (int)(gridDim.x / 2);                                            \
+    if (sb_ >= 0 && sb_ < 8 && lane == 0) g_ap_stamps[(sb_ * 4 + wave) * AP_NST + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#elif defined(MMPFN_STAMPS_ALL)  // every wave of the grid: HW_ID, XCC_ID and 36 stamps (diagnostics only)
+constexpr int AP_NST = 36, AP_MAXB = 8192;
+__device__ unsigned long long g_ap_all[AP_MAXB * 4 * (AP_NST + 2)];
+#define AP_STAMP(k)                                                                                     \
+  do {                                                                                                  \
+    if (lane == 0 && blockIdx.x < AP_MAXB && (k) < AP_NST)                                              \
+      g_ap_all[((size_t)blockIdx.x * 4 + wave) * (AP_NST + 2) + 2 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define AP_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 constexpr int P4_KT = 64;    // keys per tile
 constexpr int P4_NCH = 2;    // 32-query chains per wave
@@ -93,9 +123,9 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 }
 
 // exact two-pass softmax for one query per lane, K / V^T straight from global memory (backstop)
-template <typename QT>
+template <typename QT, typename OT>
 __device__ __attribute__((noinline)) void p4_exact_rows(const Attn2Args& p, const QT* Kg, const bf16* Vg,
-                                                        const QT* qrow, QT* orow, bool valid, float c) {
+                                                        const QT* qrow, OT* orow, bool valid, float c) {
   float q[32], o[32];
 #pragma unroll
   for (int d = 0; d < 32; ++d) q[d] = (float)qrow[d] * c, o[d] = 0.f;
@@ -119,15 +149,16 @@ __device__ __attribute__((noinline)) void p4_exact_rows(const Attn2Args& p, cons
   if (valid) {
     const float inv = 1.0f / l;
 #pragma unroll
-    for (int d = 0; d < 32; ++d) orow[d] = (QT)(o[d] * inv);
+    for (int d = 0; d < 32; ++d) orow[d] = (OT)(o[d] * inv);
   }
 }
 
-template <int F8, bool QF16>
+template <int F8, bool QF16, bool OF16>
 __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
-  typedef typename Op16<QF16>::t QT;    // Q, K and O elements
+  typedef typename Op16<QF16>::t QT;    // Q and K elements
   typedef typename Op16<QF16>::x8 Q8;
-  typedef typename Op16<QF16>::x4 Q4;
+  typedef typename Op16<OF16>::t OT;    // O elements
+  typedef typename Op16<OF16>::x4 O4;
   // LDS slot: K [64][32] bf16 in 80-B rows | V^T [32][64] in 144-B rows (bf16) or 80-B rows (e4m3)
   constexpr int VROW = F8 ? 80 : 144;
   constexpr int P4_SLOT_BYTES = 64 * 80 + 32 * VROW;
@@ -135,6 +166,14 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
+  AP_STAMP(0);
+#ifdef MMPFN_STAMPS_ALL
+  if (lane == 0 && blockIdx.x < AP_MAXB) {
+    const size_t b0 = ((size_t)blockIdx.x * 4 + wave) * (AP_NST + 2);
+    g_ap_all[b0] = __builtin_amdgcn_s_getreg(4 | (31 << 11));       // HW_REG_HW_ID
+    g_ap_all[b0 + 1] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+  }
+#endif
 
   // ---- task: the queries that read KV sequence (column b, kv head g) are the own-head rows [a0, a0+na)
   //      of head g, then, for g == kvb, rows [b0, b0+nb) of all H heads, cut into tasks of 256 (4 waves
@@ -198,8 +237,12 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     }
   }
 
+  AP_STAMP(1);
   const int ntiles = (p.nk + P4_KT - 1) / P4_KT;
   const int nfull = p.nk / P4_KT;
+#ifdef MMPFN_STAMPS
+  if (blockIdx.x == gridDim.x / 2 && tid == 0) g_ap_meta[0] = gridDim.x, g_ap_meta[1] = ntiles, g_ap_meta[2] = blockIdx.x;
+#endif
   const bool partial = nfull != ntiles;
   // key-tile order of the fast pass: the partial last tile first -- staged by the prologue with its keys
   // >= nk zeroed (K rows 0: s = 0, p = 1 exactly; V^T 0: nothing added to O) -- then tiles 0 .. nfull-1,
@@ -503,6 +546,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     gload(tile_of(min(2, ntiles - 1)), rk[0], rv[0]);
     if constexpr (LEAD == 2) gload(tile_of(min(3, ntiles - 1)), rk[1], rv[1]);
     lds_barrier();
+    AP_STAMP(2);
     if (!active) {
       // a wave without queries (a kv sequence's last, partial task) stages its share of every tile and
       // meets every barrier, but issues none of the loop's MFMAs / exps: they would take issue slots
@@ -581,6 +625,9 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       pv(0, pa, vf[B]);
       pin_step(false);
       lds_barrier();
+#if defined(MMPFN_STAMPS) || defined(MMPFN_STAMPS_ALL)
+      if (t < AP_NST - 6) AP_STAMP(3 + t);
+#endif
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -600,6 +647,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     if (ntiles & 1) pv(1, pz, vf[1]);
     else pv(1, pz, vf[0]);
   }
+  AP_STAMP(AP_NST - 3);
 
   if (!active) return;
   // ---- one tile, not pipelined, straight from global memory: every tile of the rare re-run with a
@@ -673,13 +721,14 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       for (int t = 0; t < ntiles; ++t) tile1(t, t == 0, true);
     }
   }
+  AP_STAMP(AP_NST - 2);
 
   // ---- row sums to the query's lanes, overflow backstop, normalise, store
 #pragma unroll
   for (int qb = 0; qb < P4_NCH; ++qb) {
     const float ls = rowsum(qb);
     const QRow q = qrow_of(qb);
-    QT* orow = (QT*)p.o + ((int64_t)b * p.S + q.s) * (p.H * 32) + q.h * 32;
+    OT* orow = (OT*)p.o + ((int64_t)b * p.S + q.s) * (p.H * 32) + q.h * 32;
     if (__any((__float_as_uint(ls) & 0x7fffffffu) >= 0x71800000u)) {
       const QT* qrow = (const QT*)p.q + (((int64_t)b * p.H + q.h) * p.S + q.s) * 32;
       p4_exact_rows(p, Kg, Vg, qrow, orow, q.ok && hh == 0, p.q_prescaled ? 1.0f : c);
@@ -690,9 +739,9 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     u32x2 w[4];
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq) {
-      Q4 v;
+      O4 v;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (QT)(o[qb][4 * gq + e] * inv);
+      for (int e = 0; e < 4; ++e) v[e] = (OT)(o[qb][4 * gq + e] * inv);
       w[gq] = __builtin_bit_cast(u32x2, v);
     }
 #pragma unroll
@@ -703,28 +752,45 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       if (q.ok) *(u32x4*)(orow + 8 * gg + 8 * hh) = st;
     }
   }
+  AP_STAMP(AP_NST - 1);
 }
 
 }  // namespace
 
 namespace {
-template <bool QF16>
+template <bool QF16, bool OF16>
 hipError_t launch_pipe(const Attn2Args& a, hipStream_t st) {
   if (a.f8 == 1) {
     if (!a.vt8) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((attn_pipe_kernel<1, QF16>), dim3(a.nblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_pipe_kernel<1, QF16, OF16>), dim3(a.nblocks), dim3(256), 0, st, a);
   } else if (a.f8 == 2) {
     if (!a.vt8) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((attn_pipe_kernel<2, QF16>), dim3(a.nblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_pipe_kernel<2, QF16, OF16>), dim3(a.nblocks), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((attn_pipe_kernel<0, QF16>), dim3(a.nblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_pipe_kernel<0, QF16, OF16>), dim3(a.nblocks), dim3(256), 0, st, a);
   }
   return hipGetLastError();
 }
 }  // namespace
 
+#ifdef MMPFN_STAMPS
+extern "C" int mmpfn_dbg_attn_stamps(unsigned long long* stamps, int* meta) {
+  hipError_t e = hipMemcpyFromSymbol(stamps, HIP_SYMBOL(g_ap_stamps), sizeof(g_ap_stamps));
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(meta, HIP_SYMBOL(g_ap_meta), sizeof(g_ap_meta));
+  return (int)e;
+}
+#endif
+
+#ifdef MMPFN_STAMPS_ALL
+extern "C" int mmpfn_dbg_attn_stamps_all(unsigned long long* out, int nblocks) {
+  const size_t n = (size_t)(nblocks < AP_MAXB ? nblocks : AP_MAXB) * 4 * (AP_NST + 2) * sizeof(unsigned long long);
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ap_all), n);
+}
+#endif
+
 hipError_t launch_attn_pipe(const Attn2Args& a, hipStream_t st) {
-  return a.qk_f16 ? launch_pipe<true>(a, st) : launch_pipe<false>(a, st);
+  if (a.qk_f16) return launch_pipe<true, true>(a, st);
+  return a.o_f16 ? launch_pipe<false, true>(a, st) : launch_pipe<false, false>(a, st);
 }
 
 namespace {

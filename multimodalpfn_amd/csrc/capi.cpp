@@ -501,6 +501,10 @@ GemmArgs gargs() {
 // whether PREC_F16's layer kernels take this model / table: E = 192 in 6 heads and at most 64 tokens per row
 // (T < 0: a row-wise sublayer, no token limit).  Everything else runs PREC_BF16 -- the forward (embed) and the
 // per-sublayer taps (state_tap) apply the same rule.
+#ifndef MMPFN_F16_QK_BF16
+#define MMPFN_F16_QK_BF16 1  // PREC_F16's item Q / K in bf16 (0: fp16, S on the f16 MFMA; a diagnostics variant)
+#endif
+
 inline bool f16_fits(const mmpfn_model_desc& d, int T) { return d.emsize == 192 && d.nhead == 6 && T <= 64; }
 
 // member m (of M, all of the geometry set by member 0) -> X[m] = embedded input [T][S][E]
@@ -666,8 +670,9 @@ int item_sublayer(mmpfn_ctx* ctx, int l, void* Xv, int S, int T, int N, int Npad
   const int64_t RM = (int64_t)S * T * M;  // tokens of the batch
   const int TM = T * M;                   // token columns of the batch (attention batches)
   float* Xall = (float*)Xv;
-  // PREC_F16 runs the bf16 mode's kernels in their F16 forms (fp16 X, Q, K, O; bf16 V^T)
-  const bool h16 = prec == PREC_F16;
+  // PREC_F16 runs the bf16 mode's kernels in their F16 forms (fp16 X and O; bf16 Q, K (qkb) and V^T: the
+  // attention's MFMAs all bf16)
+  const bool h16 = prec == PREC_F16, qkb = h16 && MMPFN_F16_QK_BF16;
   if (h16 && E != 192) return fail(ctx, MMPFN_ERR_INVALID, "PREC_F16 needs E = 192");
   if (h16) prec = PREC_BF16;
   const bool bf = prec == PREC_BF16;
@@ -685,7 +690,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, void* Xv, int S, int T, int N, int Npad
     const unsigned char* Vc = Kc + kvl;
     if (bf && E == 192) {
       HIPCHK(launch_rowgemm_qkv(Xv, S, S, 1, 0, h16 ? L.item_qtest_f.p : L.item_qtest_h.p, TM * S, E, Qi, Ki, Vi, S,
-                                Npad, H, st, h16));
+                                Npad, H, st, h16, qkb));
     } else if (proj3_ok(ctx, prec)) {
       const Proj3Set ps = p3set(ctx, L.item_qtest, Xall, S, S, 1, 0, (int64_t)TM * S, E);
       HIPCHK(launch_proj3_qkv(&ps, 1, Qi, Ki, Vi, S, Npad, H, st));
@@ -700,7 +705,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, void* Xv, int S, int T, int N, int Npad
     const int64_t cstride = (int64_t)cc->Npad * 32;
     if (bf)
       HIPCHK(launch_attn_layer(Qi, Kc, Vc, O, S, TM, H, cc->Npad, cc->N, 0, 0, 0, S, 0, st, cstride, true, nullptr, 0,
-                               h16));
+                               h16 && !qkb, h16));
     else
       HIPCHK(launch_attn_item(Qi, Kc, Vc, O, S, TM, H, cc->Npad, 0, S, cc->N, 0, prec, st, cstride));
   } else {
@@ -708,7 +713,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, void* Xv, int S, int T, int N, int Npad
       // train rows q|k|v and test rows q in one launch (test-row blocks last)
       HIPCHK(launch_rowgemm_qkv_pair(Xv, N, 0, h16 ? L.item_qkv_f.p : L.item_qkv_h.p, TM * N, 3 * E, Q, N,
                                      h16 ? L.item_qtest_f.p : L.item_qtest_h.p, TM * Q, E, S, Qi, Ki, Vi, S, Npad, H, st,
-                                     h16));
+                                     h16, qkb));
     } else if (proj3_ok(ctx, prec)) {  // train rows q|k|v and test rows q in one launch
       const Proj3Set ps[2] = {p3set(ctx, L.item_qkv, Xall, N, S, 1, 0, (int64_t)TM * N, 3 * E),
                               p3set(ctx, L.item_qtest, Xall, Q > 0 ? Q : 1, S, 1, N, (int64_t)TM * Q, E)};
@@ -755,7 +760,7 @@ int item_sublayer(mmpfn_ctx* ctx, int l, void* Xv, int S, int T, int N, int Npad
         HIPCHK(launch_vt_fp8(Vi, V8, (int64_t)TM * H * Npad * 32, st));
       }
       if (ev) HIPCHK(hipEventRecord(ev[0], st));
-      HIPCHK(launch_attn_layer(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st, 0, true, V8, f8, h16));
+      HIPCHK(launch_attn_layer(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st, 0, true, V8, f8, h16 && !qkb, h16));
       if (ev) HIPCHK(hipEventRecord(ev[1], st));
     } else if (prec == PREC_F32) {  // parity mode: split-bf16 products, train and test rows in one launch
       HIPCHK(launch_attn_item3(Qi, Ki, Vi, O, S, TM, H, Npad, N, 0, N, N, Q, 0, st));

@@ -111,13 +111,13 @@ hipError_t launch_mlp_rows(void* X, const void* W1perm, const void* W2perm, int6
 //   f16_row_perm order (weight_pack.h)
 hipError_t launch_rowgemm_qkv(const void* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
                               const void* W, int M, int N, void* q, void* k, void* vt, int S, int Npad, int H,
-                              hipStream_t st, bool f16 = false);
+                              hipStream_t st, bool f16 = false, bool qk_bf16 = false);  // qk_bf16: f16 X, bf16 Q / K
 // two row sets (train rows: q|k|v, test rows: q) of the same token columns in ONE launch,
 // rows m -> memory row (m / rdiv) * a_rmul + m % rdiv + roff of each set
 hipError_t launch_rowgemm_qkv_pair(const void* X, int64_t rdiv1, int64_t roff1, const void* W1, int M1, int N1,
                                    int64_t rdiv2, int64_t roff2, const void* W2, int M2, int N2, int64_t a_rmul,
                                    void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st,
-                                   bool f16 = false);
+                                   bool f16 = false, bool qk_bf16 = false);
 // C = (ln ? LayerNorm(A) : A) . W^T + bias: A fp32, bf16 or fp16 (a_f16) [M][192], W [N][192] bf16, C bf16 [M][N], N % 64 == 0;
 // with CT: outputs [vt_from, N) transposed per group of Mk rows into CT [M / Mk][N - vt_from][Mk] (Mk % 32 == 0),
 // C then [M][vt_from]
@@ -190,7 +190,8 @@ struct Attn2Args {
   int q_prescaled;     // Q already carries log2(e)/sqrt(32) (folded into the engine's bf16 Q weights)
   const unsigned char* vt8;  // f8 != 0: V^T in e4m3, the layout of vt
   int f8;              // P.V on fp8 MFMA: 0 off (bf16), 1 P in e4m3, 2 P in e5m2 (attention_pipe.hip)
-  int qk_f16;          // PREC_F16: q, k and o hold fp16 (S on f16 MFMA); vt stays bf16
+  int qk_f16;          // q, k and o hold fp16 (S on f16 MFMA; the fp16 tap); vt stays bf16
+  int o_f16;           // PREC_F16's forward: q, k bf16, o fp16 (every MFMA a bf16 one)
 };
 // software-pipelined bf16 sample-axis attention (attention_pipe.hip); tasks of ATTN_ITEM_QPB queries
 constexpr int ATTN_ITEM_QPB = 256;
@@ -205,7 +206,7 @@ hipError_t launch_attn_pipe(const Attn2Args& a, hipStream_t st);
 hipError_t launch_attn_layer(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0,
                              bool q_prescaled = false,  // Q already scaled by log2(e)/sqrt(32)
-                             const void* vt8 = nullptr, int f8 = 0, bool qk_f16 = false);
+                             const void* vt8 = nullptr, int f8 = 0, bool qk_f16 = false, bool o_f16 = false);
 // bf16 -> e4m3 (saturating) of n elements (n % 8 == 0): the F8 attention's V^T operand
 hipError_t launch_vt_fp8(const void* vt, void* vt8, int64_t n, hipStream_t st);
 // parity mode (PREC_F32) of launch_attn_layer on fp32 Q / K / V^T (split bf16 three-product MFMAs), fp32 O

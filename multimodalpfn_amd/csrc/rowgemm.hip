@@ -176,11 +176,12 @@ constexpr int OVST = 32 + 8;    // V^T tile row stride (bf16): 80 B
 constexpr int OWEL = QC * OVST; // per-wave staging elements (>= 32 * OQST)
 static_assert(32 * OQST <= OWEL, "Q/K staging tile must fit");
 
-template <bool F16>
+// QKB: Q / K stored in bf16 whatever the operand type (the fp16 mode's forward: its attention runs S on bf16 MFMA)
+template <bool F16, bool QKB>
 __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int bid, uint16_t* Ws) {
-  typedef typename Op16<F16>::t OT;  // Q / K element
+  typedef typename Op16<F16 && !QKB>::t OT;  // Q / K element
   typedef typename Op16<F16>::x8 X8;
-  typedef typename Op16<F16>::x4 X4;
+  typedef typename Op16<F16 && !QKB>::x4 X4;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
   const int rd = (int)p.a_rdiv;
@@ -317,12 +318,12 @@ __device__ __forceinline__ void qkv2_tile(const RgArgs& p, int tiles_per_b, int 
 // Two row sets in one launch: blocks [0, nblk1) project p's rows (the train rows: q|k|v), the
 // rest p2's (the test rows: q only, a third of the chunks) -- the short test-row blocks run last
 // and fill the grid's tail instead of a separate under-filled launch.
-template <bool F16>
+template <bool F16, bool QKB>
 __global__ __launch_bounds__(256, 2) void rowgemm_qkv2_kernel(const RgArgs p, int tiles_per_b, const RgArgs p2,
                                                               int tiles2, int nblk1) {
   __shared__ __attribute__((aligned(16))) uint16_t Ws[2 * QCEL + 4 * OWEL];
-  if ((int)blockIdx.x < nblk1) qkv2_tile<F16>(p, tiles_per_b, blockIdx.x, Ws);
-  else qkv2_tile<F16>(p2, tiles2, blockIdx.x - nblk1, Ws);
+  if ((int)blockIdx.x < nblk1) qkv2_tile<F16, QKB>(p, tiles_per_b, blockIdx.x, Ws);
+  else qkv2_tile<F16, QKB>(p2, tiles2, blockIdx.x - nblk1, Ws);
 }
 
 // C[m] = (LN? LayerNorm(A[m]) : A[m]) . W^T + bias, A fp32 [M][192], W [N][192] bf16, C bf16 [M][N]
@@ -564,22 +565,23 @@ hipError_t qkv_rowset(const void* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_r
 
 hipError_t launch_rowgemm_qkv(const void* X, int64_t a_rdiv, int64_t a_rmul, int64_t a_rmul2, int64_t a_roff,
                               const void* W, int M, int N, void* q, void* k, void* vt, int S, int Npad, int H,
-                              hipStream_t st, bool f16) {
+                              hipStream_t st, bool f16, bool qk_bf16) {
   RgArgs a;
   int tiles;
   int64_t nblk;
   hipError_t e = qkv_rowset(X, a_rdiv, a_rmul, a_rmul2, a_roff, W, M, N, q, k, vt, S, Npad, H, a, tiles, nblk);
   if (e != hipSuccess || nblk == 0) return e;
-  if (f16)
-    hipLaunchKernelGGL(rowgemm_qkv2_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, st, a, tiles, a, tiles, (int)nblk);
-  else
-    hipLaunchKernelGGL(rowgemm_qkv2_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, st, a, tiles, a, tiles, (int)nblk);
+  const dim3 g((unsigned)nblk);
+  if (f16 && qk_bf16) hipLaunchKernelGGL((rowgemm_qkv2_kernel<true, true>), g, dim3(256), 0, st, a, tiles, a, tiles, (int)nblk);
+  else if (f16) hipLaunchKernelGGL((rowgemm_qkv2_kernel<true, false>), g, dim3(256), 0, st, a, tiles, a, tiles, (int)nblk);
+  else hipLaunchKernelGGL((rowgemm_qkv2_kernel<false, false>), g, dim3(256), 0, st, a, tiles, a, tiles, (int)nblk);
   return hipGetLastError();
 }
 
 hipError_t launch_rowgemm_qkv_pair(const void* X, int64_t rdiv1, int64_t roff1, const void* W1, int M1, int N1,
                                    int64_t rdiv2, int64_t roff2, const void* W2, int M2, int N2, int64_t a_rmul,
-                                   void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st, bool f16) {
+                                   void* q, void* k, void* vt, int S, int Npad, int H, hipStream_t st, bool f16,
+                                   bool qk_bf16) {
   RgArgs a1, a2;
   int t1, t2;
   int64_t n1, n2;
@@ -589,10 +591,10 @@ hipError_t launch_rowgemm_qkv_pair(const void* X, int64_t rdiv1, int64_t roff1, 
   if (e != hipSuccess) return e;
   if (n1 + n2 == 0) return hipSuccess;
   if (n1 == 0) a1 = a2, t1 = t2;  // blocks index the second set only
-  if (f16)
-    hipLaunchKernelGGL(rowgemm_qkv2_kernel<true>, dim3((unsigned)(n1 + n2)), dim3(256), 0, st, a1, t1, a2, t2, (int)n1);
-  else
-    hipLaunchKernelGGL(rowgemm_qkv2_kernel<false>, dim3((unsigned)(n1 + n2)), dim3(256), 0, st, a1, t1, a2, t2, (int)n1);
+  const dim3 g((unsigned)(n1 + n2));
+  if (f16 && qk_bf16) hipLaunchKernelGGL((rowgemm_qkv2_kernel<true, true>), g, dim3(256), 0, st, a1, t1, a2, t2, (int)n1);
+  else if (f16) hipLaunchKernelGGL((rowgemm_qkv2_kernel<true, false>), g, dim3(256), 0, st, a1, t1, a2, t2, (int)n1);
+  else hipLaunchKernelGGL((rowgemm_qkv2_kernel<false, false>), g, dim3(256), 0, st, a1, t1, a2, t2, (int)n1);
   return hipGetLastError();
 }
 

@@ -61,11 +61,13 @@ def _blocks(body: str) -> list[collections.Counter]:
     return out
 
 
-@pytest.mark.parametrize("qk,smfma", [("Lb0E", "v_mfma_f32_32x32x16_bf16"), ("Lb1E", "v_mfma_f32_32x32x16_f16")])
+@pytest.mark.parametrize("qk,smfma", [("Lb0ELb0E", "v_mfma_f32_32x32x16_bf16"), ("Lb0ELb1E", "v_mfma_f32_32x32x16_bf16"),
+                                      ("Lb1ELb1E", "v_mfma_f32_32x32x16_f16")])
 def test_attention_tile_bodies_have_no_register_shuffles(qk, smfma):
     """The pipelined loop (attention_pipe.hip) is one basic block of four tiles: per tile 64 v_exp_f32,
-    32 v_cvt_pk_bf16_f32, 16 + 8 MFMAs and a handful of address / loop ops, no register shuffles (bf16 Q / K,
-    and the fp16 Q / K of PREC_F16, whose 8 score MFMAs per tile are the f16 form)."""
+    32 v_cvt_pk_bf16_f32, 16 + 8 MFMAs and a handful of address / loop ops, no register shuffles (bf16 Q / K with
+    bf16 or fp16 O -- the bf16 and the fp16 mode's forward --, and the fp16 Q / K of the kernel-level tap, whose
+    8 score MFMAs per tile are the f16 form)."""
     body = _function(_asm("attention_pipe.hip", ["-fno-honor-nans"]), f"attn_pipe_kernelILi0E{qk}")
     pvm = "v_mfma_f32_32x32x16_bf16"
     loops = [c for c in _blocks(body) if c["v_exp_f32_e32"] >= 256 and c["v_exp_f32_e32"] % 64 == 0
@@ -85,7 +87,7 @@ def test_fp8_attention_tile_bodies(variant, cvt):
     """The fp8 P.V variants (config E): per tile 64 exps, 8 score MFMAs (bf16), one 32x32x64 P.V and one
     16x16x128 row-sum MFMA per chain (block-scaled f8f6f4), 32 scaled conversions, no register shuffles
     (a defined `old` word of the packed conversions once cost 16 v_mov per tile)."""
-    body = _function(_asm("attention_pipe.hip", ["-fno-honor-nans"]), f"attn_pipe_kernelILi{variant}ELb0E")
+    body = _function(_asm("attention_pipe.hip", ["-fno-honor-nans"]), f"attn_pipe_kernelILi{variant}ELb0ELb1E")
     loops = [c for c in _blocks(body) if c["v_exp_f32_e32"] >= 256 and c["v_exp_f32_e32"] % 64 == 0
              and c["v_mfma_f32_32x32x16_bf16"] * 8 == c["v_exp_f32_e32"]]
     assert len(loops) == 1, [(c["v_exp_f32_e32"], c["v_mfma_f32_32x32x16_bf16"]) for c in _blocks(body)]
