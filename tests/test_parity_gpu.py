@@ -824,8 +824,8 @@ def test_f16_falls_back_to_bf16_on_wide_tables():
 
 F16_CASES = sorted(p.stem for p in (GOLDEN / "f16").glob("*.npz"))
 F16_REF_FACTOR = 3.0  # the fp16 mode's deviation from the fp32 reference <= 3x the reference's own fp16 deviation
-# (measured 0.68-2.16x over the nine fixtures with the MGM head bank on fp16 operands; 3.17x at image_only while it ran
-# on bf16 operands)
+# (measured 0.60-2.72x over the nine fixtures: MGM head bank on fp16 operands, item Q / K in bf16; 0.68-2.16x with fp16
+# item Q / K; 3.17x at image_only while the head bank ran on bf16 operands)
 
 
 def _load_f16_case(name):
