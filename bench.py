@@ -173,12 +173,14 @@ def time_item_attention(eng, T, reps, S=S_ROWS, N=N_TRAIN, precision=None):
     Npad = (N + 63) // 64 * 64
     dev = eng.device
     precision = _lib.PREC_BF16 if precision is None else precision
-    qk_dt = torch.float16 if precision in (_lib.PREC_F16, _lib.PREC_F16_F8, _lib.PREC_F16_F8E5) else torch.bfloat16
+    f16 = precision in (_lib.PREC_F16, _lib.PREC_F16_F8, _lib.PREC_F16_F8E5)
+    if f16:  # the fp16 mode's forward form (bf16 q / k, fp16 out), as the engine launches it
+        precision |= _lib.ATTN_QK_BF16
     g = torch.Generator(device="cpu").manual_seed(0)
-    q = torch.randn(T, H, S, d, generator=g).to(dev, qk_dt)
-    k = torch.randn(T, H, Npad, d, generator=g).to(dev, qk_dt)
+    q = torch.randn(T, H, S, d, generator=g).to(dev, torch.bfloat16)
+    k = torch.randn(T, H, Npad, d, generator=g).to(dev, torch.bfloat16)
     vt = torch.randn(T, H, d, Npad, generator=g).to(dev, torch.bfloat16)
-    o = torch.empty(T, S, H * d, device=dev, dtype=qk_dt)
+    o = torch.empty(T, S, H * d, device=dev, dtype=torch.float16 if f16 else torch.bfloat16)
     lib, ctx = eng.lib, eng.ctx
     eng._bind_stream()
     stream = torch.cuda.current_stream(dev)

@@ -62,8 +62,8 @@ extern "C" {
 #define MMPFN_PREC_BF16_F8E5 4 /* as MMPFN_PREC_BF16_F8 with P in e5m2 (wider range, 2 mantissa bits) */
 #define MMPFN_PREC_F16 5      /* the reference's fp16 autocast (utils.py:150-190, layer.py:60-62): the state X kept in
                                   fp16 between kernels, every layer contraction on fp16 MFMA operands (the item
-                                  attention's P.V on bf16), fp32 accumulation / LayerNorm / softmax statistics;
-                                  tables of more than 64 tokens per row run MMPFN_PREC_BF16 */
+                                  attention's Q / K and P.V on bf16), fp32 accumulation / LayerNorm / softmax
+                                  statistics; tables of more than 64 tokens per row run MMPFN_PREC_BF16 */
 #define MMPFN_PREC_F16_F8 6   /* MMPFN_PREC_F16 with the fp8 P.V of MMPFN_PREC_BF16_F8 */
 #define MMPFN_PREC_F16_F8E5 7 /* MMPFN_PREC_F16 with the fp8 P.V of MMPFN_PREC_BF16_F8E5 */
 
@@ -176,7 +176,9 @@ int mmpfn_item_attention_layer(mmpfn_ctx* ctx, const void* q, const void* k, con
 
 /* mmpfn_item_attention_layer in a 16-bit precision code: MMPFN_PREC_BF16 (as mmpfn_item_attention_layer),
  * MMPFN_PREC_F16 (q, k and out in fp16, vt bf16), or either with the fp8 P.V (MMPFN_PREC_*_F8: P e4m3,
- * *_F8E5: P e5m2; vt is the bf16 V^T, converted to e4m3 inside). */
+ * *_F8E5: P e5m2; vt is the bf16 V^T, converted to e4m3 inside).  A code 5-7 OR MMPFN_ATTN_QK_BF16 runs the
+ * fp16 mode's forward form: q and k in bf16 (as the engine writes them), out fp16. */
+#define MMPFN_ATTN_QK_BF16 0x100
 int mmpfn_item_attention_layer_ex(mmpfn_ctx* ctx, const void* q, const void* k, const void* vt, void* out, int S,
                                   int T, int H, int Npad, int N, int precision);
 

@@ -29,6 +29,7 @@ PREC_BF16_F8E5 = 4  # the same with P in e5m2
 PREC_F16 = 5       # the reference's fp16 autocast: fp16 state between kernels, fp16 MFMA operands, fp32 statistics
 PREC_F16_F8 = 6    # PREC_F16 with the fp8 P.V (P e4m3)
 PREC_F16_F8E5 = 7  # PREC_F16 with the fp8 P.V (P e5m2)
+ATTN_QK_BF16 = 0x100  # mmpfn_item_attention_layer_ex: code 5-7 | this = the fp16 forward's form (bf16 q / k, fp16 out)
 
 
 def f32_precision() -> int:

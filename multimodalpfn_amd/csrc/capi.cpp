@@ -1382,7 +1382,10 @@ int mmpfn_item_attention_layer_ex(mmpfn_ctx* ctx, const void* q, const void* k, 
   if (!ctx || !q || !k || !vt || !out) return MMPFN_ERR_INVALID;
   if (N <= 0 || N > S || N > Npad || Npad % 64 || H <= 0 || H > 8 || T <= 0)
     return fail(ctx, MMPFN_ERR_INVALID, "bad attention geometry");
-  if (!prec_ok(precision) || !prec16(base_prec(precision))) return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
+  const bool qkb = (precision & MMPFN_ATTN_QK_BF16) != 0;  // the fp16 forward's form: bf16 q / k, fp16 out
+  precision &= ~MMPFN_ATTN_QK_BF16;
+  if (!prec_ok(precision) || !prec16(base_prec(precision)) || (qkb && base_prec(precision) != PREC_F16))
+    return fail(ctx, MMPFN_ERR_INVALID, "bad precision");
   HIPCHK(hipSetDevice(ctx->device));
   const int f8 = f8_of(precision);
   if (f8) {
@@ -1390,8 +1393,9 @@ int mmpfn_item_attention_layer_ex(mmpfn_ctx* ctx, const void* q, const void* k, 
     RC(ensure(ctx, ctx->tap_v8, (size_t)n));
     HIPCHK(launch_vt_fp8(vt, ctx->tap_v8.p, n, ctx->stream));
   }
+  const bool h16 = base_prec(precision) == PREC_F16;
   HIPCHK(launch_attn_layer(q, k, vt, out, S, T, H, Npad, N, 0, N, N, S - N, 0, ctx->stream, 0, false,
-                           f8 ? ctx->tap_v8.p : nullptr, f8, base_prec(precision) == PREC_F16));
+                           f8 ? ctx->tap_v8.p : nullptr, f8, h16 && !qkb, h16));
   return MMPFN_OK;
 }
 

@@ -164,6 +164,7 @@ def _attn_ref(q, k, v):
 
 # parity (split bf16), bf16, fp32-input MFMA, fp8 P.V with P e4m3 / e5m2 (V^T e4m3); |O| <= ~1
 # (fp8: x max(1, max |V|) in test_item_attention_layer_fp8; measured max 0.125 at N = 1, |V| <= 3.6)
+QK_BF16 = 0x100  # _lib.ATTN_QK_BF16: the fp16 forward's form of the layer tap (bf16 Q / K, fp16 O)
 ATTN_TOL = {0: 5e-5, 1: 2e-2, 2: 2e-5, 3: 1e-1, 4: 1e-1, 5: 2e-2, 6: 1e-1, 7: 1e-1}  # 3 / 4 / 6 / 7: the
 # overflow / re-run tests (exact path); the fp8 results themselves: _f8_layer_ref, F8_QBAND
 
@@ -233,15 +234,16 @@ def _launch_layer(q, k, v, Npad, N, prec=1):
     vt[:, :, :, :N] = v.transpose(-1, -2)
     lib = _lib.load_library()
     ctx = lib.mmpfn_create(0, None)
-    dt = torch.bfloat16 if prec in (1, 3, 4, 5, 6, 7) else torch.float32
+    dt = torch.bfloat16 if prec & 0xff in (1, 3, 4, 5, 6, 7) else torch.float32
     qd, kd, vd = q.to("cuda", dt), kp.to("cuda", dt), vt.to("cuda", dt)
     out = torch.zeros(T, S, H * d, device="cuda", dtype=dt)
     if prec == 1:
         assert lib.mmpfn_item_attention_layer(ctx, qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), S, T,
                                               H, Npad, N) == 0
-    elif prec in (3, 4, 5, 6, 7):  # fp8 P.V (P e4m3: 3 / 6, e5m2: 4 / 7); 5-7: fp16 Q / K / O
-        if prec >= 5:
-            qd, kd = q.to("cuda", torch.float16), kp.to("cuda", torch.float16)
+    elif prec & 0xff in (3, 4, 5, 6, 7):  # fp8 P.V (P e4m3: 3 / 6, e5m2: 4 / 7); 5-7: fp16 Q / K / O
+        if prec & 0xff >= 5:  # (| ATTN_QK_BF16: the fp16 forward's form, bf16 Q / K and fp16 O)
+            if not prec & _lib.ATTN_QK_BF16:
+                qd, kd = q.to("cuda", torch.float16), kp.to("cuda", torch.float16)
             out = out.to(torch.float16)
         assert lib.mmpfn_item_attention_layer_ex(ctx, qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), S,
                                                  T, H, Npad, N, prec) == 0
@@ -258,10 +260,12 @@ def _launch_layer(q, k, v, Npad, N, prec=1):
 
 def _layer_ref(q, k, v, N, prec=1):
     T, H, S, d = q.shape
+    qkb, prec = bool(prec & QK_BF16), prec & 0xff
     dt = torch.bfloat16 if prec in (1, 3, 4) else torch.float32
     qr, kr, vr = (t.to(dt).float() for t in (q, k, v))
-    if prec >= 5:  # fp16 Q / K, bf16 V
-        qr, kr, vr = q.half().float(), k.half().float(), v.bfloat16().float()
+    if prec >= 5:  # fp16 Q / K (bf16 in the fp16 forward's form), bf16 V
+        qk = torch.bfloat16 if qkb else torch.float16
+        qr, kr, vr = q.to(qk).float(), k.to(qk).float(), v.bfloat16().float()
     ref_tr = _attn_ref(qr[:, :, :N], kr, vr)
     ref_te = _attn_ref(qr[:, :, N:], kr[:, :1].expand_as(kr), vr[:, :1].expand_as(vr))
     return torch.cat([ref_tr, ref_te], 2).permute(0, 2, 1, 3).reshape(T, S, H * d)
@@ -290,7 +294,8 @@ def _f8_layer_ref(q, k, v, N, prec):
     the FIRST tile processed (the partial last tile when N % 64 != 0, else tile 0), e = clamp(floor(max) - ETOP,
     -EMAX if partial else -100, 100); P' = fp8(exp2(s) / 2^e) in e4m3 / e5m2; O = sum P' V8 / sum P'."""
     T, H, S, d = q.shape
-    qk_dt = torch.float16 if prec >= 5 else torch.bfloat16
+    qkb, prec = bool(prec & QK_BF16), prec & 0xff
+    qk_dt = torch.float16 if prec >= 5 and not qkb else torch.bfloat16
     c = math.log2(math.e) / math.sqrt(d)
     qs = (q.to(qk_dt).float() * c).to(qk_dt).double()
     ks = k.to(qk_dt).double()
@@ -319,13 +324,14 @@ def _f8_outcomes(got, q, k, v, N, prec):
     T, H, S, d = q.shape
     got = got.double()
     e_q = (got - _f8_layer_ref(q, k, v, N, prec)).reshape(T, S, H, d).abs().amax(-1)
-    e_x = (got - _layer_ref(q, k, v, N, 5 if prec >= 5 else 1)).reshape(T, S, H, d).abs().amax(-1)
+    e_x = (got - _layer_ref(q, k, v, N, (5 | (prec & QK_BF16)) if prec & 0xff >= 5 else 1)).reshape(T, S, H, d)
+    e_x = e_x.abs().amax(-1)
     # (a P past the format converts to NaN / inf in the quantising reference too: that row's fp8 outcome does not
     # exist, the kernel re-ran it -- fmin takes the exact outcome there)
     return torch.fmin(e_q, e_x), (~(e_q <= e_x)).double().mean().item()
 
 
-@pytest.mark.parametrize("prec", [3, 4, 6, 7])
+@pytest.mark.parametrize("prec", [3, 4, 6, 7, 6 | QK_BF16, 7 | QK_BF16])
 @pytest.mark.parametrize("S,N,T", [(2298, 1838, 2), (70, 1, 2), (130, 64, 1), (200, 65, 3), (700, 333, 1),
                                    (12000, 10000, 1)])
 def test_item_attention_layer_fp8(S, N, T, prec):
@@ -340,13 +346,13 @@ def test_item_attention_layer_fp8(S, N, T, prec):
     vmax = v.abs().max().item()
     print(f"attention fp8 prec {prec} S={S} N={N} T={T}: max {err.max():.3e} (max|V| {vmax:.2f}), re-run {rerun:.3f}")
     assert err.max().item() < F8_QBAND * vmax
-    if N >= 1838 and prec in (4, 7):  # e5m2 P: the fp8 pass itself is what runs at the configs' sizes
+    if N >= 1838 and prec & 0xff in (4, 7):  # e5m2 P: the fp8 pass itself is what runs at the configs' sizes
         assert rerun < 0.5
     # (e4m3 P holds 9 octaves below the first tile's max: at these sizes the underflow guard sends ~every wave
     # to the exact path -- measured 1.0 at S = 2298 -- so e4m3 P is correct but not faster)
 
 
-@pytest.mark.parametrize("prec", [3, 4, 6, 7])
+@pytest.mark.parametrize("prec", [3, 4, 6, 7, 6 | QK_BF16, 7 | QK_BF16])
 def test_item_attention_fp8_wide_score_spread(prec):
     """Scores spread wide (the ATT_SCALE = 2 situation of DESIGN 5.5, here x5): later key tiles overflow the first
     tile's fp8 scale for some queries, whose waves re-run on the exact bf16 path.  Every output (row, head) must be
@@ -362,7 +368,7 @@ def test_item_attention_fp8_wide_score_spread(prec):
     assert rerun > 0.0
 
 
-@pytest.mark.parametrize("prec", [3, 4, 6, 7])
+@pytest.mark.parametrize("prec", [3, 4, 6, 7, 6 | QK_BF16, 7 | QK_BF16])
 @pytest.mark.parametrize("N", [1000, 10000])
 def test_item_attention_fp8_underflow_guard(prec, N):
     """one large score in the (first-processed) partial key tile and every other key ~11 octaves
@@ -377,18 +383,18 @@ def test_item_attention_fp8_underflow_guard(prec, N):
     k[:, :, N - 1] = u * 4.0 * 1.41        # the partial tile's last key: s = 16 * 1.41 * log2(e) / sqrt(32) ~ 5.75
     k[:, :, : N - 1] -= u * 10.6           # every other key ~ -11 log2 units: 2^-11 each, (N - 1) 2^-11 in total
     got = _launch_layer(q, k, v, Npad, N, prec).double()
-    exact = _layer_ref(q, k, v, N, 5 if prec >= 5 else 1)
+    exact = _layer_ref(q, k, v, N, (5 | (prec & QK_BF16)) if prec & 0xff >= 5 else 1)
     qref = _f8_layer_ref(q, k, v, N, prec)
     err, lost = (got - exact).abs().max().item(), (qref - exact).abs().max().item()
     print(f"underflow guard prec {prec} N={N}: max err vs exact {err:.3e} (the flushed fp8 result: {lost:.3e})")
     assert torch.isfinite(got).all()
-    if prec in (3, 6):  # e4m3: the far keys flush under the first tile's scale; the guard must re-run the waves
+    if prec & 0xff in (3, 6):  # e4m3: the far keys flush under the first tile's scale; the guard must re-run the waves
         assert err < 2e-2
     else:  # e5m2 holds them (22 octaves below its scale): the quantised result stands
         assert (got - qref).abs().max().item() < F8_QBAND * v.abs().max().item()
 
 
-@pytest.mark.parametrize("prec", [1, 0, 3, 4, 5])
+@pytest.mark.parametrize("prec", [1, 0, 3, 4, 5, 5 | QK_BF16])
 def test_item_attention_overflow_backstop(prec):
     """Scores that jump far past the first key tile's max (p would overflow the fixed
     softmax reference) take the exact two-pass recompute and still match."""
@@ -400,7 +406,7 @@ def test_item_attention_overflow_backstop(prec):
     got = _launch_layer(q, k, v, Npad, N, prec)
     ref = _layer_ref(q, k, v, N, prec)
     assert torch.isfinite(got).all()
-    assert (got.double() - ref).abs().max().item() < ATTN_TOL[prec]
+    assert (got.double() - ref).abs().max().item() < ATTN_TOL[prec & 0xff]
 
 
 @pytest.mark.parametrize("prec", [1, 0, 3, 4])

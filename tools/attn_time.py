@@ -18,23 +18,25 @@ Npad = (N + 63) // 64 * 64
 lib = _lib.load_library(os.environ.get("MMPFN_LIB") or None)
 ctx = lib.mmpfn_create(0, None)
 g = torch.Generator().manual_seed(0)
-# ATT_PREC=f16: the fp16 mode's kernel (q, k, out fp16, V^T bf16; the headline's launch), else bf16
+# ATT_PREC=f16: the fp16 mode's forward kernel (q, k bf16, out fp16, V^T bf16; the headline's launch; ATT_FORM=tap:
+# the fp16 q / k form of the kernel-level tap instead), else bf16
 f16 = os.environ.get("ATT_PREC", "bf16") == "f16"
-qdt = torch.float16 if f16 else torch.bfloat16
+tap16 = f16 and os.environ.get("ATT_FORM") == "tap"
+qdt = torch.float16 if tap16 else torch.bfloat16
 q = torch.randn(T, H, S, d, generator=g).cuda()
 k = torch.randn(T, H, Npad, d, generator=g).cuda()
 if os.environ.get("ATT_QROUND") == "bf16":  # fp16 operands holding bf16 values: the same bits toggle as in bf16 mode
     q, k = q.bfloat16().float(), k.bfloat16().float()
 q, k = q.to(qdt), k.to(qdt)
 vt = torch.randn(T, H, d, Npad, generator=g).cuda().bfloat16()
-o = torch.empty(T, S, H * d, device="cuda", dtype=qdt)
+o = torch.empty(T, S, H * d, device="cuda", dtype=torch.float16 if f16 else torch.bfloat16)
 st = torch.cuda.current_stream()
 
 
 def launch():
     if f16:
         rc = lib.mmpfn_item_attention_layer_ex(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), S, T, H,
-                                               Npad, N, 5)  # MMPFN_PREC_F16
+                                               Npad, N, 5 if tap16 else 5 | _lib.ATTN_QK_BF16)  # MMPFN_PREC_F16
     else:
         rc = lib.mmpfn_item_attention_layer(ctx, q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), S, T, H,
                                             Npad, N)
