@@ -74,6 +74,22 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
 // (the prologue's residual is the bias, its LayerNorm moves to the end beside the FFN, exact-erf GELU);
 // the vectors [bo | b0 | g | b + b3] sit in LDS beside the rings (capb, CAPL floats).
 constexpr int CAPL = 5 * RE;  // bo, b0 (2 RE), g, b + b3
+
+#ifdef MMPFN_STAMPS_ALL  // every wave of the grid: HW_ID, XCC_ID and MR_NST s_memtime stamps (diagnostics only;
+// tools/mlp_stamps_all.py): 0 start, 1 O / X / Wout half 0 landed, 2 out-projection half 0, 3 half 1, 4 LayerNorm and
+// W1(0) landed, 5 H(0), 6 + c after chunk c (c < 24), MR_NST - 1 after the stores
+constexpr int MR_NST = 32, MR_MAXB = 4096;
+__device__ unsigned long long g_mr_all[MR_MAXB * 8 * (MR_NST + 2)];
+#define MR_STAMP(k)                                                                                     \
+  do {                                                                                                  \
+    if (!CAP && lane == 0 && blockIdx.x < MR_MAXB && (k) < MR_NST)                                      \
+      g_mr_all[((size_t)blockIdx.x * NW + wave) * (MR_NST + 2) + 2 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define MR_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 template <int TT, bool RES, int NW, bool F16, bool CAP = false>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_rows_kernel(void* __restrict__ Xv,
                                                                        const void* __restrict__ W1v,
@@ -95,6 +111,14 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
   __shared__ __attribute__((aligned(1024))) bf16 lds[LDS_B / 2];
   __shared__ __attribute__((aligned(16))) float capl[CAP ? CAPL : 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  MR_STAMP(0);
+#ifdef MMPFN_STAMPS_ALL
+  if (!CAP && lane == 0 && blockIdx.x < MR_MAXB) {
+    const size_t b0 = ((size_t)blockIdx.x * NW + wave) * (MR_NST + 2);
+    g_mr_all[b0] = __builtin_amdgcn_s_getreg(4 | (31 << 11));       // HW_REG_HW_ID
+    g_mr_all[b0 + 1] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+  }
+#endif
   if constexpr (CAP)  // before any LDS-DMA: the compiler's own vmcnt waits cover these loads alone
     for (int i = tid; i < CAPL; i += 64 * NW) capl[i] = capb[i];
   const int wg = wave & 3;                           // the wave's share of a ring fill
@@ -237,6 +261,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     };
     wait_vm(integral_constant<int, 9>{});  // half 0 (and O, X) landed; half 1 may fly
     __syncthreads();
+    MR_STAMP(1);
     if constexpr (CAP)  // the out-projection accumulates onto its bias
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt)
@@ -244,6 +269,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
         for (int f = 0; f < RE / 16; ++f) y[f][tt] = *(const f32x4*)(capl + f * 16 + fg * 4);
     outproj(integral_constant<int, 0>{});
     __syncthreads();  // every wave is done with half 0: the W1 ring is free
+    MR_STAMP(2);
     dma_w1(0, 0);
     if (nchunks > 1) dma_w1(1, 1);
     if (deep) dma_w1(2, 2);
@@ -253,6 +279,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     __syncthreads();
     outproj(integral_constant<int, 1>{});
     __syncthreads();  // the W2 ring is free
+    MR_STAMP(3);
     dma_w2(0, 0);
     if (nchunks > 1) dma_w2(1, 1);
     // residual (already in y) + LayerNorm (layer.py:437-455), packed as the MLP's A^T fragments
@@ -313,6 +340,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
     else wait_vm(integral_constant<int, 0>{});
   }
   __syncthreads();
+  MR_STAMP(4);
 
   // GELU of one adjacent pair q (0 .. 4 TT - 1: tile tt, half ht, elements 2 (q & 1) + 0, 1) of a chunk's
   // H^T accumulators, packed into its bf16 B fragment for the down-projection
@@ -386,6 +414,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
   if (deep) wait_vm(integral_constant<int, MP>{});
   else wait_vm(integral_constant<int, 0>{});
   __syncthreads();
+  MR_STAMP(5);
 
   // one chunk c (PAR = c % 3): reads W1(c+1) from W1 slot (c+1)%3 and W2(c) from W2 slot c%3;
   // refills W1 slot c%3 (W1(c), read in chunk c-1) with W1(c+3) and W2 slot (c+2)%3 (W2(c-1)) with
@@ -440,6 +469,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
       }
       __syncthreads();
     }
+#ifdef MMPFN_STAMPS_ALL
+    if (c < MR_NST - 7) MR_STAMP(6 + c);
+#endif
   };
   // unrolled by three so that every ring slot is a compile-time offset (no peeled copies: the last
   // chunk's "no successor" is a uniform branch)
@@ -500,6 +532,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
       }
     }
   }
+  MR_STAMP(MR_NST - 1);
 }
 
 }  // namespace
@@ -509,6 +542,13 @@ template <bool F16>
 hipError_t launch_mr(void* X, const void* W1, const void* W2, int64_t M, int Fh, float eps, hipStream_t st,
                      const void* O, const void* Wout);
 }  // namespace
+
+#ifdef MMPFN_STAMPS_ALL
+extern "C" int mmpfn_dbg_mlp_stamps_all(unsigned long long* out, int nblocks) {
+  const size_t n = (size_t)(nblocks < MR_MAXB ? nblocks : MR_MAXB) * 8 * (MR_NST + 2) * sizeof(unsigned long long);
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mr_all), n);
+}
+#endif
 
 hipError_t launch_cap_tail(const void* O, const void* Wout, const void* W1perm, const void* W2perm, const float* vecs,
                            float* out, int64_t M, int E, float eps, hipStream_t st) {
