@@ -764,11 +764,11 @@ def main():
     lanes = eng.lanes if args.lanes is None else args.lanes
     T_launch = T * min(batch, len(mine))
 
-    def live_pass(stp):
+    def live_pass(stp, t_launch=T_launch):
         eng.lib.mmpfn_kernel_timing(eng.ctx, 1)
         dt_l = timed_steps(stp, args.steps, 1, world, device)
         eng.lib.mmpfn_kernel_timing(eng.ctx, 0)
-        r = live_roofline(eng.lib, eng.ctx, T_launch) if rank == 0 else None
+        r = live_roofline(eng.lib, eng.ctx, t_launch) if rank == 0 else None
         if r is not None:
             r["timing"] += f"; a separate pass of {args.steps} steps ({dt_l / args.steps * 1e3:.3f} ms per step)"
         return r
@@ -783,6 +783,14 @@ def main():
                 "lanes overlap, so a launch shares the GPU with the other lane's kernels",
                 "one lane: launches run one after another, as in `bench.py --lanes 1`")
             live["in_step_overlapped"] = {k: live_ovl[k] for k in ("achieved", "frac", "per_launch_ms", "timing")}
+        if batch == 1 and len(mine) >= 2:
+            # the same kernel at the two-member launch shape rounds 1-4 reported (T = 72: twice the blocks per
+            # launch, so a smaller share of the grid's last round); the step itself runs one member per launch
+            # because the two lanes then overlap each other's grid tails
+            live_b2 = live_pass(make_step(eng, members, mine, assignment, rank, img, prec, 1, 2), 2 * T)
+            if live is not None and live_b2 is not None:
+                live["two_member_launch_one_lane"] = {k: live_b2[k] for k in ("achieved", "frac", "per_launch_ms",
+                                                                             "traffic")}
 
     # ---- the other 16-bit mode (bf16 operands on an fp32 state, or the fp16 mode), same step
     other16 = None

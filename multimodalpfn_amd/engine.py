@@ -76,7 +76,7 @@ def target_uniques(y_train: np.ndarray) -> np.ndarray:
 
 
 DEFAULT_LANES = int(os.environ.get("MMPFN_LANES", "2"))  # concurrent member lanes of forward_many
-DEFAULT_BATCH = int(os.environ.get("MMPFN_BATCH", "2"))  # members per batched forward of forward_many
+DEFAULT_BATCH = int(os.environ.get("MMPFN_BATCH", "1"))  # members per batched forward of forward_many (1: DESIGN 7)
 _DEBUG_SYNC = os.environ.get("MMPFN_DEBUG_SYNC") == "1"  # diagnostics: serialise forward_many's units
 _DEBUG_KEEP = os.environ.get("MMPFN_DEBUG_KEEP") == "1"  # diagnostics: keep every prepared input alive
 _KEEP: list = []
