@@ -862,7 +862,7 @@ int decode(mmpfn_ctx* ctx, float* logits, int M = 1) {
 // tok16: the tokens in 16-bit (the MGM+CAP chain's intermediate; bf16, or fp16 under PREC_F16; E = 192 only).
 // PREC_F16 runs the head bank on fp16 operands (LN output, GLU hidden, weights) where the big-tile kernels take
 // the shape, else in the bf16 mode: fp16's 3 extra mantissa bits cut the mixer's share of the logits error ~7x
-// (DESIGN 5.8), and the reference's own fp16 autocast runs these linears in fp16.
+// (DESIGN 3, 6), and the reference's own fp16 autocast runs these linears in fp16.
 bool mgm_f16(const mmpfn_ctx* ctx) { return ctx->mgm_w1_f.p != nullptr && ctx->d.nhid % 64 == 0; }
 
 int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, void* mtok, int prec, bool tok16 = false) {
