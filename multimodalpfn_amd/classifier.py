@@ -17,6 +17,8 @@ from collections.abc import Sequence
 from pathlib import Path
 from typing import Any, Literal
 
+import os
+
 import numpy as np
 import torch
 from sklearn.base import BaseEstimator, ClassifierMixin, check_is_fitted
@@ -266,11 +268,20 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
         if X is not None:
             X = self._encode_predict_X(X)
         logits, perms = [], []
-        for out, config in self.executor_.iter_outputs(X, image_test=image_test, device=self.device_,
-                                                       autocast=self.use_autocast_):
-            assert out.ndim == 2
-            logits.append(out)
-            perms.append(config.class_permutation)
+        ex = self.executor_
+        # the NaN / error check after the aggregation is enqueued (MMPFN_DEFER_STATUS=0: before it; A/B switch)
+        defer = hasattr(ex, "check_status") and os.environ.get("MMPFN_DEFER_STATUS", "1") != "0"
+        if defer:
+            ex._defer_status = True
+        try:
+            for out, config in ex.iter_outputs(X, image_test=image_test, device=self.device_,
+                                               autocast=self.use_autocast_):
+                assert out.ndim == 2
+                logits.append(out)
+                perms.append(config.class_permutation)
+        finally:
+            if defer:
+                ex._defer_status = False
         if any(p is None for p in perms) and not all(p is None for p in perms):
             raise ValueError("members must either all or none carry a class permutation")
         perm_arr = None if perms[0] is None else np.stack([np.asarray(p) for p in perms])
@@ -278,8 +289,11 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
         if self.balance_probabilities:
             weights = (self.class_counts_ / self.class_counts_.sum()).astype(np.float32)
         eng = self.model_.engine(logits[0].device)
-        return eng.aggregate(torch.stack(logits), perm_arr, self.n_classes_, float(self.softmax_temperature),
-                             bool(self.average_before_softmax), weights)
+        probs = eng.aggregate(torch.stack(logits), perm_arr, self.n_classes_, float(self.softmax_temperature),
+                              bool(self.average_before_softmax), weights)
+        if defer:
+            ex.check_status()
+        return probs
 
     def predict_proba(self, X, image_test: np.ndarray | None) -> np.ndarray:
         """``classifier.py:517-576``: ensemble-averaged class probabilities ``[Q, n_classes]``."""

@@ -103,6 +103,8 @@ class InferenceEngine:
     _device_cache: dict = field(default_factory=dict, repr=False)
 
     _early_tokens: tuple | None = field(default=None, repr=False)
+    _pending_status: Any = field(default=None, repr=False)
+    _defer_status: bool = field(default=False, repr=False)  # set by a caller that calls check_status() itself
     _early_mixer = False  # executors whose predict runs _run_members with self.model / self.image_train
 
     def iter_outputs(self, X, image_test, *, device: torch.device, autocast: bool) -> Iterator[tuple]:
@@ -177,9 +179,21 @@ class InferenceEngine:
 
         outs: dict[int, torch.Tensor] = dict(zip(order, eng.forward_many(items(), prec)))
         if mine:
-            eng.status()  # NaN / HIP errors of every queued member (transformer.py:727-731,790-796)
+            if self._defer_status:
+                # the caller enqueues its own device work (the aggregation) first and then calls check_status():
+                # the GPU does not idle while the host waits here
+                self._pending_status = eng
+            else:
+                eng.status()  # NaN / HIP errors of every queued member (transformer.py:727-731,790-796)
         Q = len(X) if X is not None else len(image_test)
         return gather(outs, eng.device, Q, model.cfg.n_out)
+
+    def check_status(self) -> None:
+        """The deferred ``status`` of the last member loop (``_defer_status``): waits for its streams and raises
+        ``ValueError`` on NaN input (transformer.py:727-731,790-796)."""
+        eng, self._pending_status = self._pending_status, None
+        if eng is not None:
+            eng.status()
 
     _cacheable = True  # the members' train tables and train images are fixed after fit
 
