@@ -282,18 +282,19 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
         finally:
             if defer:
                 ex._defer_status = False
-        if any(p is None for p in perms) and not all(p is None for p in perms):
-            raise ValueError("members must either all or none carry a class permutation")
-        perm_arr = None if perms[0] is None else np.stack([np.asarray(p) for p in perms])
-        weights = None
-        if self.balance_probabilities:
-            weights = (self.class_counts_ / self.class_counts_.sum()).astype(np.float32)
-        eng = self.model_.engine(logits[0].device)
-        probs = eng.aggregate(torch.stack(logits), perm_arr, self.n_classes_, float(self.softmax_temperature),
-                              bool(self.average_before_softmax), weights)
-        if defer:
-            ex.check_status()
-        return probs
+        try:
+            if any(p is None for p in perms) and not all(p is None for p in perms):
+                raise ValueError("members must either all or none carry a class permutation")
+            perm_arr = None if perms[0] is None else np.stack([np.asarray(p) for p in perms])
+            weights = None
+            if self.balance_probabilities:
+                weights = (self.class_counts_ / self.class_counts_.sum()).astype(np.float32)
+            eng = self.model_.engine(logits[0].device)
+            return eng.aggregate(torch.stack(logits), perm_arr, self.n_classes_, float(self.softmax_temperature),
+                                 bool(self.average_before_softmax), weights)
+        finally:  # also when the aggregation raised: a NaN input's ValueError takes precedence, as before
+            if defer:
+                ex.check_status()
 
     def predict_proba(self, X, image_test: np.ndarray | None) -> np.ndarray:
         """``classifier.py:517-576``: ensemble-averaged class probabilities ``[Q, n_classes]``."""

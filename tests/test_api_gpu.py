@@ -99,6 +99,29 @@ def test_early_mixer_launch(fit_mode, tmp_path, monkeypatch):
         clf.predict_proba(d["X_test"], bad)
 
 
+def test_deferred_status_survives_a_failed_aggregation(tmp_path, monkeypatch):
+    """predict_proba waits for the member loop (and checks its NaN flags) after the aggregation is enqueued
+    (``InferenceEngine.check_status``).  An error between the loop and the aggregation must still run that check
+    -- no pending wait is left behind for the next predict -- and the next predict equals a clean one."""
+    from multimodalpfn_amd.engine import HipEngine
+
+    case = _case("pad_none")
+    d = case_data(case)
+    clf = make_classifier(case, write_ckpt(case, tmp_path), inference_precision=torch.float32)
+    clf.fit(d["X_train"], d["image_train"], d["y_train"])
+    ref = clf.predict_proba(d["X_test"], d["image_test"])
+
+    def boom(*a, **k):
+        raise RuntimeError("injected")
+
+    monkeypatch.setattr(HipEngine, "aggregate", boom)
+    with pytest.raises(RuntimeError, match="injected"):
+        clf.predict_proba(d["X_test"], d["image_test"])
+    assert clf.executor_._pending_status is None and not clf.executor_._defer_status
+    monkeypatch.undo()
+    np.testing.assert_array_equal(clf.predict_proba(d["X_test"], d["image_test"]), ref)
+
+
 def test_low_memory_mode_is_reproducible(tmp_path):
     """``low_memory`` re-fits members at every predict from one fixed seed (inference.py:148)."""
     case = _case("pad_none")
