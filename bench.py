@@ -859,6 +859,10 @@ def main():
                 r = time_item_attention(eng, Tc, max(3, args.attn_reps // 4), Sc, Nc, code)
                 roof["other_configs_isolated_launch"][name + names[code]] = {
                     k: r[k] for k in ("achieved", "frac", "per_launch_ms")}
+                if code in (_lib.PREC_F16_F8, _lib.PREC_BF16_F8):
+                    roof["other_configs_isolated_launch"][name + names[code]]["note"] = (
+                        "random q / k: the e4m3 underflow guard re-runs ~every wave on the exact path (DESIGN 5.7); "
+                        "with the model's own scores the guard rarely trips: config_E's 'f16 + fp8 P.V (e4m3)' step")
     eng.close()
     cfg_d = config_d_leg(device, world, rank, args, prec) if args.config_d else None
     cfg_b = None
