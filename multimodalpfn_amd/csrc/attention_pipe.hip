@@ -13,9 +13,12 @@
 //    while the exps / conversions of unit j issue, the matrix pipe runs the S MFMAs of unit j+1
 //    and the P.V + row-sum MFMAs of unit j-1 -- nothing in a step waits on anything of the same
 //    step, and the step is one basic block whose order is pinned by sched_group_barrier;
-//  * K / V^T tiles staged once per block in a four-slot LDS ring (each thread one 16-B K and one
-//    16-B V^T chunk per tile, written a tile ahead, one s_barrier per tile with no vmcnt drain), the
-//    fragments read a step ahead of their MFMAs into two rotating register sets;
+//  * K / V^T tiles staged once per block in a four-slot LDS ring, the fragments read a step ahead of
+//    their MFMAs into two rotating register sets, one s_barrier per tile.  bf16 V^T: by LDS-DMA (each
+//    wave one 1-KB K piece and one V^T piece per tile, issued three tiles ahead into XOR-swizzled unpadded
+//    slots, the barrier waiting only for the pieces of the tile the next step reads; 3 % faster than
+//    register staging); e4m3 V^T: register staging (one 16-B K and one 8-B V^T chunk per
+//    thread, written a tile ahead into padded slots);
 //  * K rows are read in a permuted order (bits 2 and 3 of the row swapped), so the 8 keys a lane's
 //    P fragment holds are 8 consecutive keys: one 16-B V^T read per fragment, no permuted V^T image.
 // Softmax: fixed reference 0 (Q carries log2(e)/sqrt(32)), p = exp2(s), row
@@ -112,6 +115,17 @@ template <> struct P8<2> {  // e5m2 (max 57344 = 2^15.8): >= 8.8 octaves of head
 constexpr int SG_VALU = 0x2, SG_MFMA = 0x8, SG_VMEM_READ = 0x20, SG_DS_READ = 0x100, SG_DS_WRITE = 0x200,
               SG_TRANS = 0x400;
 
+// K / V^T staging of the bf16-V^T kernels by LDS-DMA (no staging registers, no ds_write), 0: register staging
+#ifndef P4_DMA
+#define P4_DMA 1
+#endif
+__device__ __forceinline__ void p4_dma16(uint32_t voff, const void* sbase, unsigned lds_dst) {
+  // m0 = the wave's LDS destination; lane i's 16 B (sbase + voff) land at m0 + 16 i.  In inline asm so the
+  // compiler's waitcnt pass adds no vmcnt(0) for it; the loop waits for its own pieces at the tile barrier
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_dst)
+               : "memory");
+}
+
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -159,10 +173,13 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   typedef typename Op16<QF16>::x8 Q8;
   typedef typename Op16<OF16>::t OT;    // O elements
   typedef typename Op16<OF16>::x4 O4;
-  // LDS slot: K [64][32] bf16 in 80-B rows | V^T [32][64] in 144-B rows (bf16) or 80-B rows (e4m3)
-  constexpr int VROW = F8 ? 80 : 144;
-  constexpr int P4_SLOT_BYTES = 64 * 80 + 32 * VROW;
-  __shared__ __attribute__((aligned(16))) unsigned char ring[4 * P4_SLOT_BYTES];
+  // LDS slot: K [64][32] bf16 in 80-B rows | V^T [32][64] in 144-B rows (bf16) or 80-B rows (e4m3);
+  // DMA (bf16 V^T): K in 64-B rows | V^T in 128-B rows, unpadded and XOR-swizzled (see the fragments below)
+  constexpr bool DMA = F8 == 0 && P4_DMA;
+  constexpr int KROW = DMA ? 64 : 80;
+  constexpr int VROW = F8 ? 80 : (DMA ? 128 : 144);
+  constexpr int P4_SLOT_BYTES = 64 * KROW + 32 * VROW;
+  __shared__ __attribute__((aligned(1024))) unsigned char ring[4 * P4_SLOT_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
@@ -262,15 +279,23 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   //   F8: V^T A operand of the 32x32x64 MFMA: lane (r = d, hh) <- V^T[d][logical k 32hh .. 32hh+31], logical
   //       k 32hh + 8j + b = key 16j + 8hh + b (the keys of the P bytes, see expc): an e4m3 V^T row is stored
   //       with key group g (8 keys) at byte 32 (g & 1) + 8 (g >> 1), so a lane reads 32 contiguous bytes
-  constexpr int KROW = 80, VBASE = 64 * KROW;
+  //   DMA: the LDS-DMA writes a wave's 1 KB lane-linearly, so the padding goes and 16-B unit u of K row R sits at
+  //       u ^ ((R >> 2) & 3), of V^T row d at u ^ ((d >> 1) & 7): the 16 rows of a ds_read_b128 lane group (16
+  //       distinct rows mod 16, pk permuting only inside them) then cover all 16 16-B slots of the 256-B bank row
+  constexpr int VBASE = 64 * KROW;
   const int kb = (32 * 0 + pkr) * KROW + 16 * hh, vb = VBASE + r * VROW + (F8 ? 32 : 16) * hh;
   int kro[2][2], vro[2][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      kro[u][i] = kb + 32 * u * KROW + 32 * i;
-      vro[u][i] = vb + 64 * u + 32 * i;
+      if constexpr (DMA) {
+        kro[u][i] = (32 * u + pkr) * KROW + 16 * ((2 * i + hh) ^ ((pkr >> 2) & 3));
+        vro[u][i] = VBASE + r * VROW + 16 * ((4 * u + 2 * i + hh) ^ ((r >> 1) & 7));
+      } else {
+        kro[u][i] = kb + 32 * u * KROW + 32 * i;
+        vro[u][i] = vb + 64 * u + 32 * i;
+      }
     }
   auto readk = [&](Q8(&kf)[2][2], const unsigned char* slot) __attribute__((always_inline)) {
 #pragma unroll
@@ -295,8 +320,24 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
   // staging: thread tid holds K row tid >> 2 chunk tid & 3 and V^T row tid >> 3 key group tid & 7 of a tile
   const int krow = tid >> 2, kc = tid & 3, vd = tid >> 3, vc = tid & 7;
   const int kso = krow * 32 + kc * 8, vso = vd * p.Npad + vc * 8;  // 32-bit lane offsets on wave-uniform bases
-  const int kw = krow * KROW + 16 * kc;
-  const int vw = F8 ? VBASE + vd * VROW + 32 * (vc & 1) + 8 * (vc >> 1) : VBASE + vd * VROW + 16 * vc;
+  const int kw = krow * KROW + 16 * (DMA ? kc ^ ((krow >> 2) & 3) : kc);
+  const int vw = F8    ? VBASE + vd * VROW + 32 * (vc & 1) + 8 * (vc >> 1)
+                 : DMA ? VBASE + vd * VROW + 16 * (vc ^ ((vd >> 1) & 7))
+                       : VBASE + vd * VROW + 16 * vc;
+  // DMA: wave w fills K rows 16w .. 16w+15 and V^T rows 8w .. 8w+7 of a slot (one 1-KB piece each); lane i lands at
+  // 16 i of its piece, so it fetches the logical unit the swizzle puts there
+  uint32_t kdo = 0, vdo = 0;
+  if constexpr (DMA) {
+    const int R = 16 * wave + (lane >> 2), d = 8 * wave + (lane >> 3);
+    kdo = (uint32_t)(R * 32 + 8 * ((lane & 3) ^ ((R >> 2) & 3))) * 2;
+    vdo = (uint32_t)(d * p.Npad + 8 * ((lane & 7) ^ ((d >> 1) & 7))) * 2;
+  }
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)ring;
+  auto dma = [&](int t, int slot) __attribute__((always_inline)) {  // tile t -> ring slot (wave-uniform)
+    p4_dma16(kdo, Kg + (int64_t)t * (P4_KT * 32), __builtin_amdgcn_readfirstlane(lds0 + slot * P4_SLOT_BYTES + wave * 1024));
+    p4_dma16(vdo, Vg + t * P4_KT,
+             __builtin_amdgcn_readfirstlane(lds0 + slot * P4_SLOT_BYTES + VBASE + wave * 1024));
+  };
   // staging registers: P4_LEAD = 1: one set, tile t+3 loaded in step t and written to LDS in step t+1;
   // P4_LEAD = 2: two sets (tile j in set j & 1), tile t+4 loaded in step t, written in step t+2, so a load has
   // two steps to land instead of one (ablation: the K / V^T global loads cost ~40 us of a 258 us launch)
@@ -333,9 +374,10 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       v = __builtin_bit_cast(u32x4, e);
     }
   };
-  // one barrier per tile: the LDS writes done (lgkmcnt(0)), global loads left in flight
+  // one barrier per tile: the LDS writes done (lgkmcnt(0)), global loads left in flight; DMA: also the wave's
+  // pieces of the tile the next step reads (all but the two issued this step: vmcnt(2))
   auto lds_barrier = [&]() __attribute__((always_inline)) {
-    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_waitcnt(DMA ? 0x0072 : 0xC07F);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -517,7 +559,7 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
     // tail: the remaining exps and the 16 conversions, then the staging traffic
     __builtin_amdgcn_sched_group_barrier(SG_TRANS, P4_PIN == 2 ? 8 : 4, 0);
     __builtin_amdgcn_sched_group_barrier(SG_VALU, 16, 0);
-    if (mem) {
+    if (mem && !DMA) {
       __builtin_amdgcn_sched_group_barrier(SG_DS_WRITE, 2, 0);
       __builtin_amdgcn_sched_group_barrier(SG_VMEM_READ, 2, 0);
     }
@@ -539,18 +581,29 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       VStage rv1;
       gload(tile_of(0), rk[0], rv[0]);
       gload(tile_of(min(1, ntiles - 1)), rk1, rv1);
+      if constexpr (DMA) dma(tile_of(min(2, ntiles - 1)), 2);  // (the partial tile, if any, is tile 0: masked here)
       if (partial) mask_pad(rk[0], rv[0]);
       lstore(ring, rk[0], rv[0]);
       lstore(ring + P4_SLOT_BYTES, rk1, rv1);
     }
-    gload(tile_of(min(2, ntiles - 1)), rk[0], rv[0]);
-    if constexpr (LEAD == 2) gload(tile_of(min(3, ntiles - 1)), rk[1], rv[1]);
+    if constexpr (!DMA) {
+      gload(tile_of(min(2, ntiles - 1)), rk[0], rv[0]);
+      if constexpr (LEAD == 2) gload(tile_of(min(3, ntiles - 1)), rk[1], rv[1]);
+    }
     lds_barrier();
     AP_STAMP(2);
     if (!active) {
       // a wave without queries (a kv sequence's last, partial task) stages its share of every tile and
       // meets every barrier, but issues none of the loop's MFMAs / exps: they would take issue slots
       // from the other block's wave on its SIMD
+      if constexpr (DMA) {
+        for (int t = 0; t < ntiles; ++t) {
+          dma(tile_of(min(t + 3, ntiles - 1)), (t + 3) & 3);
+          lds_barrier();
+        }
+        __builtin_amdgcn_s_waitcnt(0x0070);  // the last pieces landed before the wave ends
+        return;
+      }
       for (int t = 0; t < ntiles; t += LEAD) {
         lstore(ring + ((t + 2) & 3) * P4_SLOT_BYTES, rk[0], rv[0]);
         gload(tile_of(min(t + 2 + LEAD, ntiles - 1)), rk[0], rv[0]);
@@ -614,12 +667,17 @@ __global__ __launch_bounds__(256, 2) void attn_pipe_kernel(const Attn2Args p) {
       readk(kf[B], ring + S1);
       readv(vf[B], ring + S0);
       constexpr int RS = LEAD == 2 ? A : 0;  // staging set of tile t+2 (and of t+2+LEAD, loaded next)
-      lstore(ring + S2, rk[RS], rv[RS]);
-      gload(tile_of(min(t + 2 + LEAD, ntiles - 1)), rk[RS], rv[RS]);
+      if constexpr (!DMA) {
+        lstore(ring + S2, rk[RS], rv[RS]);
+        gload(tile_of(min(t + 2 + LEAD, ntiles - 1)), rk[RS], rv[RS]);
+      }
       smm(sb, kf[A], 1);
       expc(pa, sa, 0);
       pv(1, pz, vf[A]);
       pin_step(true);
+      // DMA: tile t+3 into the slot tile t-1 left (its last reads done before the previous barrier); it has
+      // this step and the next to land
+      if constexpr (DMA) dma(tile_of(min(t + 3, ntiles - 1)), (L + 3) & 3);
       smm(sa, kf[B], 0);
       expc(pz, sb, 1);
       pv(0, pa, vf[B]);
