@@ -44,6 +44,15 @@ sys.path.insert(0, str(ROOT / "tests" / "golden"))
 
 METRIC = "in-context rows/sec (support+query), PAD-UFES-20 shape, 1/2/4/8 MI355X"
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+# what each mode's MFMAs actually read (the bench line's config.operands), by dtype name
+OPERANDS = {
+    "f16": "fp16 state; fp16 MFMA operands in the feature attention, item QKV projection, MLP, out-projections and "
+           "MGM head bank; bf16 operands in the item attention (Q, K of the Q.K^T scores; P, V^T of P.V: "
+           "rowgemm_qkv2_kernel<true,true> stores bf16 Q / K / V^T for attn_pipe_kernel<0,false,true>) and in the CAP "
+           "pooler; fp32 accumulation, softmax statistics and LayerNorm",
+    "bf16": "fp32 state; bf16 MFMA operands everywhere; fp32 accumulation, softmax statistics and LayerNorm",
+    "f32": "fp32 state; split-bf16 (hi + lo, three products) MFMA operands; fp32 accumulation",
+}
 HBM_PEAK_GBS = 8000.0
 
 S_ROWS, N_TRAIN, N_FEAT, N_CAT, N_CLASSES = 2298, 1838, 21, 18, 6
@@ -921,6 +930,7 @@ def main():
                 "rows_per_member": S_ROWS,
                 "tokens_per_row": T,
                 "parallelism": f"ensemble members sharded over {world} GPU(s) + RCCL all-gather of logits",
+                "operands": OPERANDS[{_lib.PREC_F16: "f16", _lib.PREC_BF16: "bf16"}.get(prec, "f32")],
             },
             "roofline": roof,
             "whole_forward": {

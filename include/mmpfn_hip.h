@@ -216,6 +216,14 @@ void mmpfn_cache_free(mmpfn_ctx* ctx, mmpfn_cache* cache);
 int mmpfn_kernel_timing(mmpfn_ctx* ctx, int enable);
 int mmpfn_kernel_timing_read(mmpfn_ctx* ctx, double* total_ms, int64_t* launches, double* flops);
 
+/* Parity mode (PREC_F32): the item attention's key count from which it runs the measured precision budget's
+ * cheap forms instead of three split products -- an opt-in throughput mode (about 1.2x the parity
+ * step), off by default: the sweep of logits error against N on the golden models (profiles/r06/parity_n0_sweep_
+ * form*.txt) found no N from which the cheap forms keep the 1e-4 contract (multi_head_attention.py:718-729 in fp32)
+ * with 2x margin.  Process-wide; returns the previous value.  n < 0: never.  form: 1 fp16 S only, 2 two-product P.V
+ * only, 3 both, 0 keep. */
+int mmpfn_set_parity_attention_min_keys(int n, int form);
+
 /* Per-sublayer taps: one sublayer of layer `layer` on a caller-provided state, in place, on the
  * context stream (the forward itself fuses across these seams: the bf16 item-attention
  * out-projection runs inside the MLP kernel there).  X: device [T][S][E] fp32, the engine's

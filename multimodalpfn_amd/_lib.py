@@ -126,6 +126,7 @@ SIGNATURES = [
     ("mmpfn_kernel_timing_read", _i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                       ctypes.POINTER(ctypes.c_double)]),
     ("mmpfn_siphash24_rows", _i, [_vp, _i64, _i64, _vp]),
+    ("mmpfn_set_parity_attention_min_keys", _i, [_i, _i]),
 ]
 
 # include/mmpfn_modality.h (modality encoders: DINOv2 ViT, ELECTRA text tower)

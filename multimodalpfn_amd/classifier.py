@@ -262,27 +262,27 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
     def predict_proba_device(self, X, image_test: np.ndarray | None) -> torch.Tensor:
         """Class probabilities ``[Q, n_classes]`` fp32 left on the GPU (no rounding)."""
         check_is_fitted(self)
-        if image_test is not None and hasattr(self.executor_, "launch_mixer_early"):
-            # the mixer first: it does not need X, so the host's validation / encoding of X runs under it
-            self.executor_.launch_mixer_early(image_test, device=self.device_, autocast=self.use_autocast_)
-        if X is not None:
-            X = self._encode_predict_X(X)
-        logits, perms = [], []
         ex = self.executor_
         # the NaN / error check after the aggregation is enqueued (MMPFN_DEFER_STATUS=0: before it; A/B switch)
         defer = hasattr(ex, "check_status") and os.environ.get("MMPFN_DEFER_STATUS", "1") != "0"
-        if defer:
-            ex._defer_status = True
         try:
-            for out, config in ex.iter_outputs(X, image_test=image_test, device=self.device_,
-                                               autocast=self.use_autocast_):
-                assert out.ndim == 2
-                logits.append(out)
-                perms.append(config.class_permutation)
-        finally:
+            if image_test is not None and hasattr(ex, "launch_mixer_early"):
+                # the mixer first: it does not need X, so the host's validation / encoding of X runs under it
+                ex.launch_mixer_early(image_test, device=self.device_, autocast=self.use_autocast_)
+            if X is not None:
+                X = self._encode_predict_X(X)
+            logits, perms = [], []
             if defer:
-                ex._defer_status = False
-        try:
+                ex._defer_status = True
+            try:
+                for out, config in ex.iter_outputs(X, image_test=image_test, device=self.device_,
+                                                   autocast=self.use_autocast_):
+                    assert out.ndim == 2
+                    logits.append(out)
+                    perms.append(config.class_permutation)
+            finally:
+                if defer:
+                    ex._defer_status = False
             if any(p is None for p in perms) and not all(p is None for p in perms):
                 raise ValueError("members must either all or none carry a class permutation")
             perm_arr = None if perms[0] is None else np.stack([np.asarray(p) for p in perms])
@@ -292,7 +292,12 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
             eng = self.model_.engine(logits[0].device)
             return eng.aggregate(torch.stack(logits), perm_arr, self.n_classes_, float(self.softmax_temperature),
                                  bool(self.average_before_softmax), weights)
-        finally:  # also when the aggregation raised: a NaN input's ValueError takes precedence, as before
+        finally:
+            # whatever raised (X validation, the member loop, the aggregation): no early mixer tokens stay
+            # referenced, and the deferred NaN / HIP check of a member loop that ran still runs (a NaN input's
+            # ValueError takes precedence over the error in flight, as before)
+            if hasattr(ex, "_early_tokens"):
+                ex._early_tokens = None
             if defer:
                 ex.check_status()
 

@@ -20,6 +20,8 @@
 //    and combined once at the end.
 //      bf16 : v_mfma_f32_32x32x16_bf16 (4 per 32x64 score tile + 4 for P.V)
 //      f32  : v_mfma_f32_32x32x2_f32 (parity mode; exact fp32 fma chains)
+#include <atomic>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -565,7 +567,13 @@ __device__ __attribute__((noinline)) void a3_exact_rows(const Attn2Args& p, cons
   }
 }
 
+// CHEAP: the measured precision budget of DESIGN 5.7 as an opt-in (the launcher picks it when the sequence has
+// >= x3_cheap_min_keys keys, default never; profiles/r06/parity_n0_sweep_form*.txt): bit 0, S = K Q^T on ONE fp16 product (Q, K
+// rounded to fp16); bit 1, P.V on two products (P rounded to bf16 once, V split: Vl Ph + Vh Ph) and the row sums over
+// that same Ph.  CHEAP = 0: every operand split (three products each).
+template <int CHEAP>
 __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
+  constexpr bool CS = (CHEAP & 1) != 0, CPV = (CHEAP & 2) != 0;
   __shared__ __attribute__((aligned(16))) unsigned char lds[2][A3_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -597,6 +605,7 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
   int qh[A3_NCH], qsrow[A3_NCH];
   bool qok[A3_NCH];
   bf16x8 qfh[A3_NCH][2], qfl[A3_NCH][2];
+  f16x8 qf16[A3_NCH][2];
 #pragma unroll
   for (int qb = 0; qb < A3_NCH; ++qb) {
     const int j = jw + 32 * qb + r;
@@ -610,9 +619,15 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
     }
     const float* qrow = (const float*)p.q + (((int64_t)b * p.H + qh[qb]) * p.S + qsrow[qb]) * 32;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      a3_split8(*(const f32x4*)(qrow + 16 * ks + 8 * hh), *(const f32x4*)(qrow + 16 * ks + 8 * hh + 4), c,
-                qfh[qb][ks], qfl[qb][ks]);
+    for (int ks = 0; ks < 2; ++ks) {
+      const f32x4 a = *(const f32x4*)(qrow + 16 * ks + 8 * hh), e = *(const f32x4*)(qrow + 16 * ks + 8 * hh + 4);
+      if constexpr (CS) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) qf16[qb][ks][i] = (_Float16)(a[i] * c), qf16[qb][ks][4 + i] = (_Float16)(e[i] * c);
+      } else {
+        a3_split8(a, e, c, qfh[qb][ks], qfl[qb][ks]);
+      }
+    }
   }
 
   const int ntiles = (p.nk + A2_KT - 1) / A2_KT;
@@ -639,9 +654,16 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
   auto lstore = [&](int buf) __attribute__((always_inline)) {
     unsigned char* Ks = lds[buf];
     bf16x8 hi, lo;
-    a3_split8(rk[0], rk[1], 1.0f, hi, lo);
-    *(bf16x8*)(Ks + koff_w) = hi;
-    *(bf16x8*)(Ks + 4096 + koff_w) = lo;
+    if constexpr (CS) {  // K in fp16, one plane
+      f16x8 kk;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) kk[i] = (_Float16)rk[0][i], kk[4 + i] = (_Float16)rk[1][i];
+      *(f16x8*)(Ks + koff_w) = kk;
+    } else {
+      a3_split8(rk[0], rk[1], 1.0f, hi, lo);
+      *(bf16x8*)(Ks + koff_w) = hi;
+      *(bf16x8*)(Ks + 4096 + koff_w) = lo;
+    }
     a3_split8(rv[0], rv[1], 1.0f, hi, lo);
     const u32x4 vh = __builtin_bit_cast(u32x4, hi), vl = __builtin_bit_cast(u32x4, lo);
     *(u32x2*)(Ks + 8192 + voff_w0) = u32x2{vh.x, vh.y};
@@ -685,12 +707,17 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
     const unsigned char* Ks = lds[it & 1];
     if (active) {
       bf16x8 kh[2][2], kl[2][2], vh[2][2], vl[2][2];
+      f16x8 k16[2][2];
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          kh[u][i] = *(const bf16x8*)(Ks + kro[u][i]);
-          kl[u][i] = *(const bf16x8*)(Ks + 4096 + kro[u][i]);
+          if constexpr (CS) {
+            k16[u][i] = *(const f16x8*)(Ks + kro[u][i]);
+          } else {
+            kh[u][i] = *(const bf16x8*)(Ks + kro[u][i]);
+            kl[u][i] = *(const bf16x8*)(Ks + 4096 + kro[u][i]);
+          }
           vh[u][i] = *(const bf16x8*)(Ks + vro[u][i]);
           vl[u][i] = *(const bf16x8*)(Ks + 4096 + vro[u][i]);
         }
@@ -699,6 +726,11 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
       for (int qb = 0; qb < A3_NCH; ++qb)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
+          if constexpr (CS) {
+            s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k16[u][0], qf16[qb][0], zero16, 0, 0, 0);
+            s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k16[u][1], qf16[qb][1], s[qb][u], 0, 0, 0);
+            continue;
+          }
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[u][0], qfh[qb][0], zero16, 0, 0, 0);
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[u][1], qfh[qb][1], s[qb][u], 0, 0, 0);
           s[qb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[u][0], qfl[qb][0], s[qb][u], 0, 0, 0);
@@ -745,7 +777,13 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
             for (int j = 0; j < 8; ++j) {
               const float e = __builtin_amdgcn_exp2f(s[qb][u][8 * sp + j]);
               ph[j] = (bf16)e;
-              pl[j] = (bf16)(e - (float)ph[j]);
+              if constexpr (!CPV) pl[j] = (bf16)(e - (float)ph[j]);
+            }
+            if constexpr (CPV) {
+              o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl[u][sp], ph, o[qb], 0, 0, 0);
+              o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[u][sp], ph, o[qb], 0, 0, 0);
+              lacc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, ph, lacc[qb], 0, 0, 0);
+              continue;
             }
             o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl[u][sp], ph, o[qb], 0, 0, 0);
             o[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[u][sp], pl, o[qb], 0, 0, 0);
@@ -828,6 +866,20 @@ __global__ __launch_bounds__(256, 2) void attn_item3_kernel(const Attn2Args p) {
 
 
 namespace {
+// parity mode: key count from which the item attention takes a cheap form (attn_item3_kernel<1..3>: fp16 S and / or
+// two-product P.V).  Off by default (-1): the sweep of logits error against N on the golden models
+// (profiles/r06/parity_n0_sweep_form{1,2,3}.txt, N = 40 .. 1838) found no N from which either form stays 2x under the
+// 1e-4 contract (fp16 S: ~1e-4 at every N; two-product P.V: 4.3e-4 at N = 40 falling to 5.8e-5 at 1838), so the
+// cheap forms are an opt-in throughput mode (mmpfn_set_parity_attention_min_keys)
+#ifndef X3_CHEAP_MIN_KEYS
+#define X3_CHEAP_MIN_KEYS (-1)
+#endif
+#ifndef X3_CHEAP_FORM
+#define X3_CHEAP_FORM 3
+#endif
+std::atomic<int> g_x3_cheap_min_keys{X3_CHEAP_MIN_KEYS};
+std::atomic<int> g_x3_cheap_form{X3_CHEAP_FORM};  // attn_item3_kernel's CHEAP bits on those sequences
+
 hipError_t launch_item_attention(const void* q, const void* k, const void* vt, void* out, int S, int T, int H,
                                  int Npad, int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st,
                                  int64_t kv_bstride, bool q_prescaled, bool x3, const void* vt8 = nullptr,
@@ -857,7 +909,13 @@ hipError_t launch_item_attention(const void* q, const void* k, const void* vt, v
   a.nblocks = acc * T;
   if (a.nblocks == 0) return hipSuccess;
   if (x3) {
-    hipLaunchKernelGGL(attn_item3_kernel, dim3(a.nblocks), dim3(256), 0, st, a);
+    // the budget's cheap forms only on sequences long enough to average their rounding (x3_cheap_min_keys)
+    const int mk = g_x3_cheap_min_keys.load(std::memory_order_relaxed);
+    const int form = mk >= 0 && nk >= mk ? g_x3_cheap_form.load(std::memory_order_relaxed) : 0;
+    if (form == 1) hipLaunchKernelGGL(attn_item3_kernel<1>, dim3(a.nblocks), dim3(256), 0, st, a);
+    else if (form == 2) hipLaunchKernelGGL(attn_item3_kernel<2>, dim3(a.nblocks), dim3(256), 0, st, a);
+    else if (form == 3) hipLaunchKernelGGL(attn_item3_kernel<3>, dim3(a.nblocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(attn_item3_kernel<0>, dim3(a.nblocks), dim3(256), 0, st, a);
     return hipGetLastError();
   }
   return launch_attn_pipe(a, st);
@@ -870,6 +928,11 @@ hipError_t launch_attn_layer(const void* q, const void* k, const void* vt, void*
                              bool q_prescaled, const void* vt8, int f8, bool qk_f16, bool o_f16) {
   return launch_item_attention(q, k, vt, out, S, T, H, Npad, nk, a0, na, b0, nb, kvb, st, kv_bstride, q_prescaled,
                                false, vt8, f8, qk_f16, o_f16);
+}
+
+int set_x3_cheap_min_keys(int n, int form) {
+  if (form >= 1 && form <= 3) g_x3_cheap_form.store(form);
+  return g_x3_cheap_min_keys.exchange(n);
 }
 
 hipError_t launch_attn_item3(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,

@@ -138,6 +138,11 @@ int fail(mmpfn_ctx* c, int code, const std::string& msg) {
     if (rc_ != MMPFN_OK) return rc_; \
   } while (0)
 
+// the shapes the fp16 MGM head bank's big-tile kernels take (uploaded by finalize, used by mixer_mgm)
+bool mgm_f16_shape(const mmpfn_model_desc& d) {
+  return d.emsize == 192 && (d.mgm_heads * d.nhid) % 256 == 0 && d.nhid % 64 == 0;
+}
+
 int ensure(mmpfn_ctx* ctx, DevBuf& b, size_t bytes) {
   if (b.bytes >= bytes && b.p) return MMPFN_OK;
   if (b.p) HIPCHK(hipFree(b.p));
@@ -347,9 +352,15 @@ int finalize(mmpfn_ctx* ctx) {
     if ((rc = up2(ctx, ctx->mgm_w1, ctx->mgm_w1_h, W1))) return rc;
     if ((rc = upload(ctx, ctx->mgm_b1, B1, false))) return rc;
     if ((rc = up2(ctx, ctx->mgm_w2, ctx->mgm_w2_h, W2))) return rc;
-    if (E == 192 && (mg * D) % 256 == 0 && D % 64 == 0) {  // PREC_F16's head bank (the big-tile kernels only)
+    if (mgm_f16_shape(d)) {  // PREC_F16's head bank (the big-tile kernels only)
       if ((rc = upload_f16(ctx, ctx->mgm_w1_f, W1))) return rc;
       if ((rc = upload_f16(ctx, ctx->mgm_w2_f, W2))) return rc;
+    } else {  // a re-finalised context with another head count must not keep the previous model's fp16 bank
+      for (DevBuf* b : {&ctx->mgm_w1_f, &ctx->mgm_w2_f})
+        if (b->p) {
+          HIPCHK(hipFree(b->p));
+          *b = DevBuf{};
+        }
     }
     if ((rc = upload(ctx, ctx->mgm_b2, B2, false))) return rc;
   }
@@ -863,7 +874,7 @@ int decode(mmpfn_ctx* ctx, float* logits, int M = 1) {
 // PREC_F16 runs the head bank on fp16 operands (LN output, GLU hidden, weights) where the big-tile kernels take
 // the shape, else in the bf16 mode: fp16's 3 extra mantissa bits cut the mixer's share of the logits error ~7x
 // (DESIGN 3, 6), and the reference's own fp16 autocast runs these linears in fp16.
-bool mgm_f16(const mmpfn_ctx* ctx) { return ctx->mgm_w1_f.p != nullptr && ctx->d.nhid % 64 == 0; }
+bool mgm_f16(const mmpfn_ctx* ctx) { return ctx->mgm_w1_f.p != nullptr && mgm_f16_shape(ctx->d); }
 
 int mixer_mgm(mmpfn_ctx* ctx, const float* image, int S, int n_mod, void* mtok, int prec, bool tok16 = false) {
   const mmpfn_model_desc& d = ctx->d;
@@ -1345,6 +1356,8 @@ void mmpfn_cache_free(mmpfn_ctx* ctx, mmpfn_cache* cache) {
   }
   cache_release(cache);
 }
+
+int mmpfn_set_parity_attention_min_keys(int n, int form) { return mmpfn::set_x3_cheap_min_keys(n, form); }
 
 int mmpfn_kernel_timing(mmpfn_ctx* ctx, int enable) {
   if (!ctx) return MMPFN_ERR_INVALID;

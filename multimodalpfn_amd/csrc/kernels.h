@@ -210,6 +210,7 @@ hipError_t launch_attn_layer(const void* q, const void* k, const void* vt, void*
 // bf16 -> e4m3 (saturating) of n elements (n % 8 == 0): the F8 attention's V^T operand
 hipError_t launch_vt_fp8(const void* vt, void* vt8, int64_t n, hipStream_t st);
 // parity mode (PREC_F32) of launch_attn_layer on fp32 Q / K / V^T (split bf16 three-product MFMAs), fp32 O
+int set_x3_cheap_min_keys(int n, int form);  // previous value; mmpfn_set_parity_attention_min_keys
 hipError_t launch_attn_item3(const void* q, const void* k, const void* vt, void* out, int S, int T, int H, int Npad,
                              int nk, int a0, int na, int b0, int nb, int kvb, hipStream_t st, int64_t kv_bstride = 0);
 // item attention: queries s in [s0, s0+nq), keys [0, nk); kv_head_fixed >= 0 forces that KV head

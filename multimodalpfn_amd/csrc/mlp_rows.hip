@@ -42,11 +42,17 @@ constexpr int LDS_B = 2 * NSLOT * SLOT_B;  // 72 KB per block: two blocks per CU
 constexpr int MP = SLOT_B / 1024 / 4;      // 1-KB DMA pieces per wave, matrix and chunk (3)
 typedef __attribute__((ext_vector_type(2))) float float2_t;
 
+// "m0" in the clobber list: clang keeps m0 reserved and ignores the entry (-Winline-asm; the ISA is identical with
+// and without it), and every m0 use the compiler emits itself is preceded by its own write -- test_codegen checks
+// that no m0 read other than these DMA issues exists in the kernels
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void mlp_dma16(uint32_t voff, const void* sbase, unsigned lds_dst) {
   // m0 = the wave's LDS destination; lane i's 16 B (sbase + voff) land at m0 + 16 i
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_dst)
-               : "memory");
+               : "memory", "m0");
 }
+#pragma clang diagnostic pop
 
 template <typename F, int... I>
 __device__ __forceinline__ void static_for_(F&& f, std::integer_sequence<int, I...>) {

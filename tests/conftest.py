@@ -29,3 +29,14 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    try:
+        from helpers import REPORT
+    except Exception:  # noqa: BLE001
+        return
+    if REPORT:
+        terminalreporter.write_sep("-", "measured numbers")
+        for line in REPORT:
+            terminalreporter.write_line(line)

@@ -14,6 +14,15 @@ from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
 from oracle.forward import OracleSpec
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
+
+# numbers a test wants in the run's tail (conftest.pytest_terminal_summary prints them after the result line,
+# so `pytest -q` on the GPU box carries them even for passing tests)
+REPORT: list[str] = []
+
+
+def report(line: str) -> None:
+    print(line)
+    REPORT.append(line)
 CASES = sorted(p.stem for p in GOLDEN.glob("*.npz") if not p.stem.startswith(("api_", "modality_")))
 
 

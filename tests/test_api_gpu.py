@@ -121,6 +121,24 @@ def test_deferred_status_survives_a_failed_aggregation(tmp_path, monkeypatch):
     monkeypatch.undo()
     np.testing.assert_array_equal(clf.predict_proba(d["X_test"], d["image_test"]), ref)
 
+    # an error inside the member loop's consumer (after _run_members deferred its check) and one in X's
+    # validation (after the early mixer was queued): no pending check, no early tokens left behind
+    ex = clf.executor_
+    real_iter = type(ex).iter_outputs
+
+    def bad_iter(self, *a, **k):
+        for out, cfg in real_iter(self, *a, **k):
+            yield out[None], cfg  # 3-D: the loop body's shape assertion fires
+    monkeypatch.setattr(type(ex), "iter_outputs", bad_iter)
+    with pytest.raises(AssertionError):
+        clf.predict_proba(d["X_test"], d["image_test"])
+    assert ex._pending_status is None and not ex._defer_status and ex._early_tokens is None
+    monkeypatch.undo()
+    with pytest.raises(ValueError):
+        clf.predict_proba(d["X_test"][:, :1], d["image_test"])  # wrong width: X validation raises
+    assert ex._pending_status is None and ex._early_tokens is None
+    np.testing.assert_array_equal(clf.predict_proba(d["X_test"], d["image_test"]), ref)
+
 
 def test_low_memory_mode_is_reproducible(tmp_path):
     """``low_memory`` re-fits members at every predict from one fixed seed (inference.py:148)."""

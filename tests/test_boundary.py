@@ -97,3 +97,16 @@ def test_loader_refuses_variant_builds(tmp_path, monkeypatch):
     monkeypatch.setattr(_lib, "_LIB", None)
     with pytest.raises(RuntimeError, match="MMPFN_DIAGNOSTICS"):
         _lib.load_library()
+
+
+def test_parity_attention_switch_defaults_off_and_round_trips():
+    """mmpfn_set_parity_attention_min_keys: off (-1) by default -- no N keeps the cheap forms 2x under 1e-4
+    (profiles/r06/parity_n0_sweep_form*.txt) -- and returns the previous value (no GPU call)."""
+    lib = _lib.load_library()
+    prev = lib.mmpfn_set_parity_attention_min_keys(512, 2)
+    try:
+        assert prev == -1
+        assert lib.mmpfn_set_parity_attention_min_keys(0, 0) == 512
+    finally:
+        lib.mmpfn_set_parity_attention_min_keys(-1, 3)
+    assert lib.mmpfn_set_parity_attention_min_keys(-1, 0) == -1

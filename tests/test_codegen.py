@@ -175,3 +175,21 @@ def test_hot_kernels_use_no_scratch(src, extra):
     # the CAP tail (mixer, once per predict) spills row addresses once in its prologue (tests the limit above)
     bad = [(n, int(v)) for n, v in sizes if int(v) and "mlp_rows_kernelILi2ELb1ELi4ELb0ELb1E" not in n]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("src,extra", [("attention_pipe.hip", ["-fno-honor-nans"]), ("mlp_rows.hip", []),
+                                       ("gemm.hip", []), ("modality.hip", [])])
+def test_lds_dma_asm_owns_m0(src, extra):
+    """The LDS-DMA issues write m0 in inline asm.  clang keeps m0 reserved, so the asm's "m0" clobber
+    cannot stop the compiler from assuming a value of its own survives the asm; this checks that no such value
+    exists: every m0 reference in the compiled kernels is one of the asm's own writes, each followed by its DMA."""
+    lines = [ln.strip() for ln in _asm(src, extra).splitlines()]
+    ours = 0
+    for i, ln in enumerate(lines):
+        if not re.search(r"\bm0\b", ln) or ln.startswith((";", ".", "//")):
+            continue
+        assert re.match(r"s_mov_b32 m0, s\d+$", ln), ln
+        nxt = [x for x in lines[i + 1:i + 4] if x and not x.startswith(";")]
+        assert nxt[0] == "s_nop 0" and nxt[1].startswith("global_load_lds_dwordx4"), (ln, nxt)
+        ours += 1
+    assert ours > 0
