@@ -216,16 +216,27 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
         fast = getattr(self, "_ordinal_plan_", None)
         if fast is not None and isinstance(X, np.ndarray) and X.dtype.kind in "biuf" and X.ndim == 2:
             Xf = X.astype(np.float64, copy=False)
-            cols, cats, nan_seen, rem = fast
+            cols, cats, miss, lut, rem = fast
             out = np.empty((Xf.shape[0], len(cols) + len(rem)), dtype=np.float64)
-            for k, (j, c) in enumerate(zip(cols, cats)):
-                v = Xf[:, j]
-                idx = np.searchsorted(c, v)
-                idc = np.minimum(idx, max(len(c) - 1, 0))
-                hit = (idx < len(c)) & (c[idc] == v) if len(c) else np.zeros(v.shape, bool)
+            if cols:
+                v = Xf[:, cols]
+                if lut is not None:
+                    # integer categories in a small range (the usual case): one table lookup for every encoded
+                    # column at once; a value that is not an integer of the column's range is unseen (-1)
+                    lo, table = lut
+                    vi = np.floor(v)
+                    pos = vi - lo
+                    ok = (vi == v) & (pos >= 0) & (pos < table.shape[1])
+                    idx = np.where(ok, pos, 0).astype(np.intp)
+                    enc = np.where(ok, table[np.arange(len(cols)), idx], -1.0)
+                else:
+                    enc = np.empty(v.shape)
+                    for k, c in enumerate(cats):
+                        idx = np.searchsorted(c, v[:, k])
+                        hit = c[np.minimum(idx, len(c) - 1)] == v[:, k] if len(c) else np.zeros(len(v), bool)
+                        enc[:, k] = np.where(hit, idx, -1.0)
                 # missing -> NaN only if missing was a fitted category, else it is unseen (-1)
-                miss = np.nan if nan_seen[k] else -1.0
-                out[:, k] = np.where(np.isnan(v), miss, np.where(hit, idx, -1.0))
+                out[:, :len(cols)] = np.where(np.isnan(v), miss, enc)
             if rem:
                 out[:, len(cols):] = Xf[:, rem]
             return out
@@ -252,7 +263,17 @@ class MMPFNClassifier(ClassifierMixin, BaseEstimator):
             nan_seen.append(bool(np.isnan(c).any()))
             cats.append(np.sort(c[~np.isnan(c)]))
         rem = [int(c) for c in ts[1][2]] if len(ts) > 1 else []
-        self._ordinal_plan_ = (cols, cats, nan_seen, rem)
+        miss = np.array([np.nan if n else -1.0 for n in nan_seen])
+        # integer categories spanning < 4096 values: a [column][value - lo] table of category indices (-1: unseen)
+        lut = None
+        allc = np.concatenate(cats) if cats else np.zeros(0)
+        if cats and len(allc) and np.all(allc == np.floor(allc)) and allc.max() - allc.min() < 4096:
+            lo = float(allc.min())
+            table = np.full((len(cats), int(allc.max() - lo) + 1), -1.0)
+            for k, c in enumerate(cats):
+                table[k, (c - lo).astype(np.intp)] = np.arange(len(c))
+            lut = (lo, table)
+        self._ordinal_plan_ = (cols, cats, miss, lut, rem)
 
     def predict(self, X, X_image: np.ndarray | None) -> np.ndarray:
         """Arg-max class labels (``classifier.py:504-515``)."""

@@ -186,6 +186,9 @@ def test_numpy_predict_encoding_matches_pandas_route(name, tmp_path):
     g = np.random.default_rng(0)
     Xt[g.random(Xt.shape) < 0.05] = np.nan  # missing values
     Xt[0, :] = 97.0  # unseen categories
+    Xt[1, :] = -0.0  # signed zero (equal to a fitted 0.0)
+    if len(Xt) > 3:  # the categories of the next column (the vectorised search must keep columns apart)
+        Xt[2, :-1] = Xt[3, 1:]
     fast = clf._encode_predict_X(Xt)
     slow = clf.preprocessor_.transform(_fix_dtypes(validate_X_predict(Xt, clf),
                                                    cat_indices=clf.categorical_features_indices))
@@ -218,3 +221,30 @@ def test_passthrough_member_transform_fast_path(name, tmp_path):
             X = step.transform(X).X
     if name == "pad_none":
         assert seen > 0  # run.py's members take the fast path
+
+
+@pytest.mark.parametrize("scale", [1.0, 0.5])
+def test_numpy_predict_encoding_with_missing_categories_at_fit(tmp_path, scale):
+    """Categorical columns that held NaN at fit (missing is then a fitted category: NaN stays NaN) and columns that
+    did not (missing -> -1), through the numpy path against the ColumnTransformer route: integer categories take the
+    lookup table, half-integer ones (scale 0.5) the per-column search."""
+    from multimodalpfn_amd.utils import _fix_dtypes, validate_X_predict
+
+    case = _case("pad_none")
+    d = case_data(case)
+    clf = make_classifier(case, write_ckpt(case, tmp_path), device="cpu")
+    Xtr = d["X_train"].copy() * scale
+    Xtr[::7, 0] = np.nan
+    Xtr[::5, 3] = np.nan
+    clf.fit(Xtr, d["image_train"], d["y_train"])
+    if clf._ordinal_plan_ is None:
+        pytest.skip("encoder plan not numeric")
+    assert (clf._ordinal_plan_[3] is None) == (scale != 1.0)
+    Xt = d["X_test"].copy() * scale
+    Xt[::3, :] = np.nan
+    Xt[1, :] = 55.0
+    Xt[2, :] = 0.5
+    fast = clf._encode_predict_X(Xt)
+    slow = clf.preprocessor_.transform(_fix_dtypes(validate_X_predict(Xt, clf),
+                                                   cat_indices=clf.categorical_features_indices))
+    np.testing.assert_array_equal(fast, np.asarray(slow, dtype=np.float64))
