@@ -373,10 +373,11 @@ def test_item_attention_layer_fp8(S, N, T, prec):
     vmax = v.abs().max().item()
     print(f"attention fp8 prec {prec} S={S} N={N} T={T}: max {err.max():.3e} (max|V| {vmax:.2f}), re-run {rerun:.3f}")
     assert err.max().item() < F8_QBAND * vmax
-    if N >= 1838 and prec & 0xff in (4, 7):  # e5m2 P: the fp8 pass itself is what runs at the configs' sizes
-        assert rerun < 0.5
-    # (e4m3 P holds 9 octaves below the first tile's max: at these sizes the underflow guard sends ~every wave
-    # to the exact path -- measured 1.0 at S = 2298 -- so e4m3 P is correct but not faster)
+    if N >= 1838:  # the fp8 pass itself is what runs at the configs' sizes: e5m2 never re-runs;
+        # e4m3 with its first-tile max at 2^2 re-runs ~16-19 % of the waves on random q / k (measured round 6; with the
+        # max at 2^0 the underflow guard sent 92-100 % of them back)
+        assert rerun < (0.05 if prec & 0xff in (4, 7) else 0.5), rerun
+        report(f"fp8 re-run fraction prec {prec} S={S} N={N}: {rerun:.3f}")
 
 
 @pytest.mark.parametrize("prec", [3, 4, 6, 7, 6 | QK_BF16, 7 | QK_BF16])
