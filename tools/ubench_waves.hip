@@ -97,5 +97,7 @@ int main() {
   run<1, 3>("1 chain per wave, 3 waves per SIMD");
   run<1, 4>("1 chain per wave, 4 waves per SIMD");
   run<2, 3>("2 chains per wave, 3 waves per SIMD");
+  run<3, 1>("3 chains per wave, 1 wave per SIMD");
+  run<4, 1>("4 chains per wave, 1 wave per SIMD");
   return 0;
 }
