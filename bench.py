@@ -122,9 +122,10 @@ def attn_traffic(T):
     """HBM bytes per attention launch over T token columns, from the committed PMC pass
     (tools/attn_pmc.sh: rocprofv3 FETCH_SIZE and WRITE_SIZE runs at that launch shape)."""
     H, d, S, N = 6, 32, S_ROWS, N_TRAIN
-    # the shipped kernel's own pass only, newest first: the fp16 mode's launch (rounds 5, 4), then the bf16 one
+    # the shipped kernel's own pass only, newest first: the fp16 mode's launch (rounds 6, 5, 4), then the bf16 one
     # (round 3; older rounds measured attn_item2)
-    cands = sorted((ROOT / "profiles" / "r05").glob("attn_pipe_pmc_T*_f16.json")) + \
+    cands = sorted((ROOT / "profiles" / "r06").glob("attn_pipe_pmc_T*_f16.json")) + \
+        sorted((ROOT / "profiles" / "r05").glob("attn_pipe_pmc_T*_f16.json")) + \
         sorted((ROOT / "profiles" / "r04").glob("attn_pipe_pmc_T*_f16.json")) + \
         sorted((ROOT / "profiles" / "r03").glob("attn_pipe_pmc_T*[0-9].json"))
     for pmc in cands:
