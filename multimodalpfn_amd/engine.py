@@ -75,6 +75,23 @@ def target_uniques(y_train: np.ndarray) -> np.ndarray:
     return np.unique(y).astype(np.float32)
 
 
+# Lane streams are process-wide (one per device and lane index), shared by every engine: each HIP stream is bound to
+# one of the device's few hardware queues (GPU_MAX_HW_QUEUES), and two lanes that land on the same queue run one after
+# the other.  Which pool streams share a queue is not under the caller's control -- per-engine streams gave every second
+# MMPFNClassifier of a process 15.0-15.9 instead of 13.6-13.8 ms per predict at config C -- so the first pair, made
+# together at the first lanes' use, serves all engines (13.5-13.8 ms for all four classifiers of the same test;
+# profiles/r06/api_lane_streams.txt; CU-masked streams 17-24 ms, a high-priority second lane 14.0-14.8 ms).
+_LANE_STREAMS: dict = {}
+
+
+def _lane_stream(device: torch.device, k: int) -> torch.cuda.Stream:
+    key = (str(device), k)
+    st = _LANE_STREAMS.get(key)
+    if st is None:
+        st = _LANE_STREAMS[key] = torch.cuda.Stream(device)
+    return st
+
+
 DEFAULT_LANES = int(os.environ.get("MMPFN_LANES", "2"))  # concurrent member lanes of forward_many
 DEFAULT_BATCH = int(os.environ.get("MMPFN_BATCH", "1"))  # members per batched forward of forward_many (1: DESIGN 7)
 _DEBUG_SYNC = os.environ.get("MMPFN_DEBUG_SYNC") == "1"  # diagnostics: serialise forward_many's units
@@ -415,7 +432,7 @@ class HipEngine:
 
     def _lane_streams(self, n: int) -> list:
         if len(self._streams) < n:
-            self._streams += [torch.cuda.Stream(self.device) for _ in range(n - len(self._streams))]
+            self._streams += [_lane_stream(self.device, len(self._streams) + i) for i in range(n - len(self._streams))]
         return self._streams[:n]
 
     def aggregate(self, logits: torch.Tensor, perms, n_classes: int, temperature: float,
