@@ -199,3 +199,34 @@ def test_reference_cache_engine_call_form():
     assert torch.equal(o16.cpu(), f16.cpu())
     for m in members:
         m.empty_trainset_representation_cache()
+
+
+def test_engines_share_lane_streams_and_stay_exact():
+    """Lane streams are process-wide (engine._lane_stream: a second engine's own pair could land on one hardware queue
+    and run its lanes serially): two engines get the same lane streams, and members of both, launched
+    alternately on those shared lanes, equal each engine's members forwarded alone, bitwise."""
+    from synth import synth_image, synth_state_dict
+
+    from multimodalpfn_amd import _lib
+    from multimodalpfn_amd.model.spec import ModelConfig, state_dict_spec
+
+    cfg = ModelConfig(nlayers=2, mgm_heads=8, cap_heads=4)
+    e1 = _model(cfg, synth_state_dict(state_dict_spec(cfg), 5)).engine()
+    e2 = _model(cfg, synth_state_dict(state_dict_spec(cfg), 6)).engine()
+    im = torch.from_numpy(synth_image(S_ROWS, 1, 5)).cuda()
+    members = _ragged_members(4, 5, None)
+    with torch.inference_mode():
+        outs, refs = [], []
+        for eng in (e1, e2):
+            tok = eng.mixer_tokens(im, _lib.PREC_F16)
+            items = [(xm.cuda(), tok, ym) for xm, ym in members]
+            outs.append((eng, items, eng.forward_many(items, _lib.PREC_F16, lanes=2, batch=1)))
+        assert e1._lane_streams(2) == e2._lane_streams(2)
+        for eng, items, got in outs:
+            eng.status()
+            refs.append([eng.forward(x, t, y, _lib.PREC_F16) for x, t, y in items])
+        torch.cuda.synchronize()
+    for (eng, items, got), ref in zip(outs, refs):
+        for a, b in zip(got, ref):
+            assert torch.isfinite(a).all()
+            assert torch.equal(a.cpu(), b.cpu())
