@@ -871,8 +871,9 @@ def main():
                     k: r[k] for k in ("achieved", "frac", "per_launch_ms")}
                 if code in (_lib.PREC_F16_F8, _lib.PREC_BF16_F8):
                     roof["other_configs_isolated_launch"][name + names[code]]["note"] = (
-                        "random q / k: the e4m3 underflow guard re-runs ~every wave on the exact path (DESIGN 5.7); "
-                        "with the model's own scores the guard rarely trips: config_E's 'f16 + fp8 P.V (e4m3)' step")
+                        "random q / k: ~10 % of the waves fail the e4m3 range checks (first-tile scale, DESIGN 5.8) and "
+                        "repeat their queries on the exact non-pipelined path (~4x a pipelined pass); e5m2 never does; "
+                        "the model's own scores: config_E's 'f16 + fp8 P.V (e4m3)' step")
     eng.close()
     cfg_d = config_d_leg(device, world, rank, args, prec) if args.config_d else None
     cfg_b = None
