@@ -123,6 +123,67 @@ __device__ __forceinline__ f16x2_t gelu_tanh_h2(f16x2_t x) {
   return x * f16x2_t{(_Float16)__builtin_amdgcn_rcph(d[0]), (_Float16)__builtin_amdgcn_rcph(d[1])};
 }
 
+// gelu_tanh_h2 on two pairs at once, bitwise the same values.  The compiler builds each pair's exp / rcp from
+// one v_exp_f16 / v_rcp_f16 on the low half, one SDWA form reading the high half, and a v_pack_b32_f16 (2 of
+// the pair's 12 issue slots); here the SDWA form writes the high half in place (dst_sel WORD_1, preserve).
+// The two pairs alternate so that every read of a transcendental's result comes one instruction after it
+// (gfx950's one-wait-state trans-use rule, which the compiler keeps with s_nop outside asm), and the block
+// ends with non-transcendental instructions.
+__device__ __forceinline__ void gelu_tanh_h2x2(f16x2_t& a, f16x2_t& b) {
+  constexpr float k = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+  const f16x2_t kk = {(_Float16)k, (_Float16)k}, kc = {(_Float16)(k * 0.044715f), (_Float16)(k * 0.044715f)};
+  const f16x2_t ua = a * __builtin_elementwise_fma(kc, a * a, kk), ub = b * __builtin_elementwise_fma(kc, b * b, kk);
+  f16x2_t ea, eb, ra, rb;
+  asm("v_exp_f16_e32 %0, %4\n\t"
+      "v_exp_f16_e32 %1, %5\n\t"
+      "v_exp_f16_sdwa %0, %4 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+      "v_exp_f16_sdwa %1, %5 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+      "v_pk_add_f16 %0, %0, 1.0 op_sel_hi:[1,0]\n\t"
+      "v_pk_add_f16 %1, %1, 1.0 op_sel_hi:[1,0]\n\t"
+      "v_rcp_f16_e32 %2, %0\n\t"
+      "v_rcp_f16_e32 %3, %1\n\t"
+      "v_rcp_f16_sdwa %2, %0 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+      "v_rcp_f16_sdwa %3, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+      "v_pk_mul_f16 %2, %6, %2\n\t"
+      "v_pk_mul_f16 %3, %7, %3"
+      : "=&v"(ea), "=&v"(eb), "=&v"(ra), "=&v"(rb)
+      : "v"(ua), "v"(ub), "v"(a), "v"(b));
+  a = ra, b = rb;
+}
+
+// gelu_tanh_h2x2 from the four fp32 values (h0, h1) (h2, h3) themselves, conversion and the cubic included: the
+// whole two-pair chain in one block, every dependent instruction one slot behind its producer (the wait state
+// the compiler keeps after v_pk_fma_f16 and after a transcendental), so that no s_nop is needed inside and the
+// block's inputs are old accumulators (no conservative s_nop in front of it either)
+__device__ __forceinline__ void gelu_tanh_h2x2_f32(float h0, float h1, float h2, float h3, f16x2_t& a, f16x2_t& b) {
+  constexpr float k = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+  const f16x2_t kk = {(_Float16)k, (_Float16)k}, kc = {(_Float16)(k * 0.044715f), (_Float16)(k * 0.044715f)};
+  f16x2_t xa, xb, ua, ub, ra, rb;
+  asm("v_cvt_pk_f16_f32 %2, %8, %9\n\t"
+      "v_cvt_pk_f16_f32 %3, %10, %11\n\t"
+      "v_pk_mul_f16 %4, %2, %2\n\t"
+      "v_pk_mul_f16 %5, %3, %3\n\t"
+      "v_pk_fma_f16 %4, %4, %6, %7\n\t"
+      "v_pk_fma_f16 %5, %5, %6, %7\n\t"
+      "v_pk_mul_f16 %4, %2, %4\n\t"
+      "v_pk_mul_f16 %5, %3, %5\n\t"
+      "v_exp_f16_e32 %0, %4\n\t"
+      "v_exp_f16_e32 %1, %5\n\t"
+      "v_exp_f16_sdwa %0, %4 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+      "v_exp_f16_sdwa %1, %5 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+      "v_pk_add_f16 %4, %0, 1.0 op_sel_hi:[1,0]\n\t"
+      "v_pk_add_f16 %5, %1, 1.0 op_sel_hi:[1,0]\n\t"
+      "v_rcp_f16_e32 %0, %4\n\t"
+      "v_rcp_f16_e32 %1, %5\n\t"
+      "v_rcp_f16_sdwa %0, %4 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+      "v_rcp_f16_sdwa %1, %5 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+      "v_pk_mul_f16 %0, %2, %0\n\t"
+      "v_pk_mul_f16 %1, %3, %1"
+      : "=&v"(ra), "=&v"(rb), "=&v"(xa), "=&v"(xb), "=&v"(ua), "=&v"(ub)
+      : "v"(kc), "v"(kk), "v"(h0), "v"(h1), "v"(h2), "v"(h3));
+  a = ra, b = rb;
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // Reductions over the four 16-lane rows of an MFMA C fragment (lanes l, l^16, l^32, l^48):

@@ -351,7 +351,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
   // GELU of one adjacent pair q (0 .. 4 TT - 1: tile tt, half ht, elements 2 (q & 1) + 0, 1) of a chunk's
   // H^T accumulators, packed into its bf16 B fragment for the down-projection
 #ifndef MLP_GELU16
-#define MLP_GELU16 1
+#define MLP_GELU16 3  // 3: gelu_tanh_h2x2_f32, 2: gelu_tanh_h2x2, 1: one pair per gelu_tanh_h2, 0: fp32 tanh form
 #endif
   auto gelu_pair = [&](auto qc, const f32x4 (&hs)[2][TT], X8 (&hb)[TT], int c) {
     constexpr int q = decltype(qc)::value, tt = q >> 2, ht = (q >> 1) & 1, i = 2 * (q & 1);
@@ -360,6 +360,23 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (TT == 2 ? 2 : 1)) void mlp_
       const float2_t bb = *(const float2_t*)(capl + RE + c * RHC + 16 * ht + 4 * fg + i);
       pr = __builtin_convertvector((float2_t){gelu_erf(hs[ht][tt][i] + bb[0]), gelu_erf(hs[ht][tt][i + 1] + bb[1])},
                                    HT2);
+    } else if constexpr (F16 && MLP_GELU16 == 3) {  // fp16 mode: pairs q, q + 1 from the fp32 accumulators
+      if constexpr ((q & 1) == 0) {
+        f16x2_t a, b;
+        gelu_tanh_h2x2_f32(hs[ht][tt][0], hs[ht][tt][1], hs[ht][tt][2], hs[ht][tt][3], a, b);
+        hb[tt][4 * ht + 0] = a[0], hb[tt][4 * ht + 1] = a[1];
+        hb[tt][4 * ht + 2] = b[0], hb[tt][4 * ht + 3] = b[1];
+      }
+      return;
+    } else if constexpr (F16 && MLP_GELU16 == 2) {  // fp16 mode: pairs q, q + 1 (one tile row's four values) at once
+      if constexpr ((q & 1) == 0) {
+        f16x2_t a = __builtin_convertvector((float2_t){hs[ht][tt][0], hs[ht][tt][1]}, f16x2_t);
+        f16x2_t b = __builtin_convertvector((float2_t){hs[ht][tt][2], hs[ht][tt][3]}, f16x2_t);
+        gelu_tanh_h2x2(a, b);
+        hb[tt][4 * ht + 0] = a[0], hb[tt][4 * ht + 1] = a[1];
+        hb[tt][4 * ht + 2] = b[0], hb[tt][4 * ht + 3] = b[1];
+      }
+      return;
     } else if constexpr (F16 && MLP_GELU16) {  // fp16 mode: the pair's GELU in packed fp16 arithmetic
       pr = gelu_tanh_h2(__builtin_convertvector((float2_t){hs[ht][tt][i], hs[ht][tt][i + 1]}, HT2));
     } else {
