@@ -193,3 +193,31 @@ def test_lds_dma_asm_owns_m0(src, extra):
         assert nxt[0] == "s_nop 0" and nxt[1].startswith("global_load_lds_dwordx4"), (ln, nxt)
         ours += 1
     assert ours > 0
+
+
+def test_mlp_f16_gelu_asm_spacing():
+    """The fp16 MLP's GELU runs as two-pair asm blocks (common.h gelu_tanh_h2x2_f32): the high halves of the
+    v_exp_f16 / v_rcp_f16 results are written in place by SDWA (no v_pack_b32_f16 left in the kernel), and the
+    compiler cannot see inside the asm, so the block itself must keep gfx950's one wait state between a
+    transcendental (or v_pk_fma_f16) and the next instruction that reads its result (a preserving SDWA write reads
+    its destination), and must not end on a transcendental."""
+    asm = _asm("mlp_rows.hip")
+    checked = 0
+    for variant in ("Lb1E", "Lb0E"):
+        body = _function(asm, f"mlp_rows_kernelILi2E{variant}Li4ELb1ELb0E")
+        assert "v_pack_b32_f16" not in body
+        for blk in re.findall(r";;#ASMSTART\n(.*?);;#ASMEND", body, re.S):
+            ins = [ln.strip() for ln in blk.splitlines() if ln.strip().startswith("v_")]
+            if not any(i.startswith("v_exp_f16") for i in ins):
+                continue
+            checked += 1
+            regs = [re.findall(r"\bv\d+\b", i) for i in ins]
+            for k in range(1, len(ins)):
+                prev = ins[k - 1]
+                if not re.match(r"v_(exp|rcp)_f16|v_pk_fma_f16", prev):
+                    continue
+                written = regs[k - 1][0]
+                reads = regs[k][1:] + (regs[k][:1] if "UNUSED_PRESERVE" in ins[k] else [])
+                assert written not in reads, (prev, ins[k])
+            assert not re.match(r"v_(exp|rcp)_f16", ins[-1]), ins[-1]
+    assert checked >= 8, checked
