@@ -56,6 +56,18 @@ __device__ __forceinline__ X8 cat8(const f32x4& a, const f32x4& b, float s = 1.0
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// one 1-KB LDS-DMA piece in the saddr form: lane i's 16 B at sbase + voff land at LDS m0 + 16 i (a scalar base per
+// piece and one offset VGPR for all of them; the builtin's 64-bit VGPR address per piece cost ~19 VGPRs at the
+// kernel's register peak).  m0: clang keeps it reserved and ignores the clobber (-Winline-asm); test_codegen checks
+// that every m0 use in the kernels is one of these issues.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void fr_dma16(uint32_t voff, const void* sbase, unsigned lds_dst) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_dst)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 template <int NT, bool F16>
 __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* __restrict__ Xv,
                                                                          const void* __restrict__ packv, int S, int T,
@@ -65,7 +77,9 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
   typedef typename Op16<F16>::t WT;
   const WT* __restrict__ pack = (const WT*)packv;
   __shared__ __attribute__((aligned(1024))) WT wbuf[2 * FR_QKV_IMG];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (wave in an SGPR: the LDS-DMA piece addresses below are then a scalar base + the lane's 16-B offset, the
+  // saddr form, instead of one 64-bit VGPR address per piece -- 10 pieces a head, ~19 VGPRs at the peak)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = lane & 15, g = lane >> 4;
   const int row = blockIdx.x * 4 + wave;  // row over the batch: member row / S, table row row % S
   const bool rowok = row < M * S;  // wave-uniform; a wave past the last row recomputes it and stores nothing
@@ -77,19 +91,23 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
   // LDS-DMA of `pieces` KB from src (global) to dst (LDS), KB piece p by wave p % 4
   // (non-dependent pointer types: a builtin call on a template-dependent type is checked at instantiation,
   // where the host pass cannot resolve it, and the kernel's host stub is then silently dropped)
+  const uint32_t dvoff = lane * 16;
+  // the asm DMA issues are invisible to the compiler's waitcnt pass: each barrier that publishes an image waits
+  // for this wave's pieces itself (vmcnt counts them with the wave's other global loads)
+  auto dma_wait = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+  auto lds_u32 = [](const void* p) { return (unsigned)(uintptr_t)(lds_void*)p; };
   auto dma = [&](const void* srcv, void* dstv, int pieces) {
-    const uint16_t* src = (const uint16_t*)srcv;
-    uint16_t* dst = (uint16_t*)dstv;
+    const char* src = (const char*)srcv;
+    const unsigned dst = lds_u32(dstv);
     for (int p = wave; p < pieces; p += 4)
-      __builtin_amdgcn_global_load_lds(src + p * 512 + lane * 8, (lds_void*)(dst + p * 512), 16, 0, 0);
+      fr_dma16(dvoff, src + p * 1024, __builtin_amdgcn_readfirstlane(dst + p * 1024));
   };
 
   // the same copy one piece at a time: piece i of this wave (wave + 4 i), clamped to the last piece so that
   // the call is branch-free (a clamped piece rewrites the last piece's bytes with the same data)
   auto dma_piece = [&](const void* srcv, void* dstv, int i) {
     const int p = min(wave + 4 * i, FR_PIECES - 1);
-    __builtin_amdgcn_global_load_lds((const uint16_t*)srcv + p * 512 + lane * 8, (lds_void*)((uint16_t*)dstv + p * 512),
-                                     16, 0, 0);
+    fr_dma16(dvoff, (const char*)srcv + p * 1024, __builtin_amdgcn_readfirstlane(lds_u32(dstv) + p * 1024));
   };
 #ifndef FR_DMA_SPREAD
 #define FR_DMA_SPREAD 1
@@ -98,6 +116,15 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
   constexpr bool SPREAD = FR_DMA_SPREAD && F16;  // the bf16 form: +16 spilled registers, not spread
 
   dma(pack, wbuf, FR_PIECES);  // head 0 -> buffer 0
+  // fp16 row addresses: a wave-uniform row base and a 32-bit lane offset per token tile (the saddr form: one VGPR
+  // per tile where a 64-bit address per tile, live to the final stores, cost spills)
+  const char* const xrow = (const char*)(X + (int64_t)sr * FR_E);
+  uint32_t xoff[NT];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) {
+    const int t = 16 * tt + n;
+    xoff[tt] = (uint32_t)(((tt == NT - 1 && t >= T ? 0 : t) * SE + 8 * g) * sizeof(XT));
+  }
   // ---- the row's tokens as bf16 fragments (padding tokens t >= T are zero)
   X8 xf[NT][FR_E / 32];
 #pragma unroll
@@ -108,7 +135,7 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
 #pragma unroll
     for (int ks = 0; ks < FR_E / 32; ++ks) {
       if constexpr (F16) {
-        xf[tt][ks] = *(const f16x8*)(xr + 32 * ks);
+        xf[tt][ks] = *(const f16x8*)(xrow + xoff[tt] + 64 * ks);
         if (pad) xf[tt][ks] = f16x8{};
       } else {
         f32x4 lo = *(const f32x4*)(xr + 32 * ks), hi = *(const f32x4*)(xr + 32 * ks + 4);
@@ -117,7 +144,8 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
       }
     }
   }
-  __syncthreads();  // (its vmcnt(0) retires the DMA too)
+  dma_wait();
+  __syncthreads();
 
   X8 of[FR_H][NT];  // O^T fragments of every head (K-step h of the out-projection)
 #pragma unroll
@@ -222,12 +250,14 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
       of[h][qt] = cat8<X8>(oa[0], oa[1], inv);
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();  // DMA of the next image landed; this head's buffer is free
+    dma_wait();  // the next image landed (every wave's pieces: the barrier below); this head's buffer is free
+    __syncthreads();
   }
   // second half of the out-projection image (buffer 1, read by head 5 until the barrier above)
   dma(pack + FR_H * FR_QKV_IMG + FR_QKV_IMG, wbuf + FR_QKV_IMG, FR_PIECES);
   // (running token tile 0's output features 0 .. 95, buffer 0's rows, before this barrier measured neutral:
   // 101.9 / 102.4 vs 101.3 / 101.9 µs, profiles/r04/ab_feat_rows_dma_spread.txt)
+  dma_wait();
   __syncthreads();
 
   // ---- per token tile: Y^T = Wout . O^T over K = 192 (K-step h = head h), image [192][FR_ST],
@@ -284,7 +314,7 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             ov[i] = (f16)((y[2 * k][i] - mean) * rs), ov[4 + i] = (f16)((y[2 * k + 1][i] - mean) * rs);
-          *(f16x8*)(xr + 32 * k) = ov;
+          *(f16x8*)(xrow + xoff[tt] + 64 * k) = ov;
         }
       } else {
 #pragma unroll
