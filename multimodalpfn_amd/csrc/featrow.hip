@@ -116,8 +116,8 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
   constexpr bool SPREAD = FR_DMA_SPREAD && F16;  // the bf16 form: +16 spilled registers, not spread
 
   dma(pack, wbuf, FR_PIECES);  // head 0 -> buffer 0
-  // fp16 row addresses: a wave-uniform row base and a 32-bit lane offset per token tile (the saddr form: one VGPR
-  // per tile where a 64-bit address per tile, live to the final stores, cost spills)
+  // row addresses: a wave-uniform row base and a 32-bit lane offset per token tile (the saddr form: one VGPR per
+  // tile where a 64-bit address per tile, live to the final stores, cost spills); lane offset = token t, features 8 g
   const char* const xrow = (const char*)(X + (int64_t)sr * FR_E);
   uint32_t xoff[NT];
 #pragma unroll
@@ -131,14 +131,14 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
   for (int tt = 0; tt < NT; ++tt) {
     const int t = 16 * tt + n;
     const bool pad = tt == NT - 1 && t >= T;  // only the last tile holds padding (T > 16 (NT - 1))
-    const XT* xr = X + (int64_t)(pad ? 0 : t) * SE + (int64_t)sr * FR_E + 8 * g;
 #pragma unroll
     for (int ks = 0; ks < FR_E / 32; ++ks) {
       if constexpr (F16) {
         xf[tt][ks] = *(const f16x8*)(xrow + xoff[tt] + 64 * ks);
         if (pad) xf[tt][ks] = f16x8{};
       } else {
-        f32x4 lo = *(const f32x4*)(xr + 32 * ks), hi = *(const f32x4*)(xr + 32 * ks + 4);
+        const char* xr = xrow + xoff[tt] + 128 * ks;
+        f32x4 lo = *(const f32x4*)xr, hi = *(const f32x4*)(xr + 16);
         if (pad) lo = hi = f32x4{0.f, 0.f, 0.f, 0.f};
         xf[tt][ks] = cat8<X8>(lo, hi);
       }
@@ -275,7 +275,8 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
     const int t = 16 * tt + n;
     const bool pad = tt == NT - 1 && t >= T;
     const bool valid = rowok && !pad;
-    XT* xr = X + (int64_t)(pad ? 0 : t) * SE + (int64_t)sr * FR_E + (F16 ? 8 : 4) * g;
+    // fp32 state: the residual / output pieces are 4 features at 16 f + 4 g (the Y^T rows of the lane)
+    char* const xr = (char*)xrow + xoff[tt] - 16 * g;
     float sm = 0.f;
     if constexpr (F16) {  // the residual is the lane's own X fragments (image rows permuted to match)
 #pragma unroll
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
     } else {
 #pragma unroll
       for (int f = 0; f < FR_E / 16; ++f) {
-        const f32x4 xv = *(const f32x4*)(xr + 16 * f);
+        const f32x4 xv = *(const f32x4*)(xr + 64 * f);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           y[f][i] += xv[i];
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(256, NT <= 3 ? 2 : 1) void feat_rows_kernel(void* _
           f32x4 ov;
 #pragma unroll
           for (int i = 0; i < 4; ++i) ov[i] = (y[f][i] - mean) * rs;
-          *(f32x4*)(xr + 16 * f) = ov;
+          *(f32x4*)(xr + 64 * f) = ov;
         }
       }
     }
